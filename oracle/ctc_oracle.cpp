@@ -1,0 +1,458 @@
+// ctc_oracle.cpp — CPU restatement of the reference CTC beam search with
+// per-beam best-alignment tracking.
+//
+// *** TEST INFRASTRUCTURE ONLY. ***  This file is the parity checker and the
+// CPU-baseline workload.  Only tests/, __graft_entry__.smoke() and bench.py's
+// cpu_baseline leg may load it.  The product path (ctc-beam-search-op_amd/)
+// never links, loads or calls it.
+//
+// Pinning: the reference (TF custom op) is unbuildable in this image (it needs
+// TensorFlow and Eigen headers that are not installed), so this restatement is
+// pinned by the reference's own golden vector — the Graves-paper example in
+// python/ops/ctc_ext_beam_search_decoder_ops_test.py:20-100 — checked by
+// tests/test_oracle_golden.py, for T=float and T=double.  Every other parity
+// case is pinned only through this restatement.
+//
+// What is restated, with the reference lines it follows
+// (paths relative to tensorflow_ctc_ext_beam_search_decoder/cc/):
+//   * LogSumExp, kLogZero                    util/ctc_loss_util.h:19-41
+//   * BeamProbability / alignment candidates util/ctc_beam_entry.h:32-100
+//   * BeamEntry: Active/New/GetChild/LabelSeq/AlignmentLabelSeq/
+//     AddAlignmentCandidate                   util/ctc_beam_entry.h:105-246
+//   * BeamRoot arena, BeamComparer            util/ctc_beam_entry.h:248-280
+//   * Step / Reset / TopPaths                 util/ctc_ext_beam_search_decoder.h:66-261
+//   * Compute batch driver, validation, SparseTensor packing
+//                                             kernels/ctc_ext_beam_search_decoder_kernels.cc:20-257
+//   * gtl::TopN (third-party, TensorFlow tensorflow/core/lib/gtl/top_n.h,
+//     TF 1.14-2.1 era per configure.sh:59-81): restated from its published
+//     algorithm — UNORDERED -> BOTTOM_KNOWN -> HEAP_SORTED, libstdc++
+//     make_heap/pop_heap/sort_heap/std::sort (the heap layout decides
+//     tie order, so the real libstdc++ algorithms are used here).
+//
+// Two alignment stores (selected per call):
+//   kFaithful: every candidate owns a std::vector<int> label sequence kept in a
+//              std::priority_queue, copied on every AddAlignmentCandidate —
+//              the reference's data structures and O(W*C*T^2) cost.  This is
+//              the mode timed as bench.py's cpu_baseline ("port").
+//   kShared:   a candidate is (prob, index into an append-only (label, prev)
+//              arena) and only the first-pushed maximum is kept.  Same results
+//              (only .top() of each queue is ever read, ctc_beam_entry.h:92-99),
+//              O(W*C*T) cost; used for mid-size parity cases.
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <limits>
+#include <memory>
+#include <queue>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace oracle {
+
+template <class T>
+constexpr T LogZero() { return -std::numeric_limits<T>::infinity(); }
+
+// util/ctc_loss_util.h:29-41.  Float libm even when T is double.
+template <class T>
+inline T LSE(T a, T b) {
+  if (a == LogZero<T>()) return b;
+  if (b == LogZero<T>()) return a;
+  return (a > b) ? a + log1pf(expf(b - a)) : b + log1pf(expf(a - b));
+}
+
+inline float NumExp(float x) { return expf(x); }
+inline double NumExp(double x) { return exp(x); }
+inline float NumLog(float x) { return logf(x); }
+inline double NumLog(double x) { return log(x); }
+
+// ---------------------------------------------------------------------------
+// gtl::TopN restatement.
+template <class E, class Greater>
+class BoundedTop {
+ public:
+  explicit BoundedTop(size_t limit) : limit_(limit) {}
+  size_t size() const { return std::min(v_.size(), limit_); }
+  void push(E e) {
+    if (limit_ == 0) return;
+    if (state_ != kHeap) {
+      v_.push_back(e);
+      if (state_ != kUnordered && !gt_(v_.back(), v_.front())) std::swap(v_.front(), v_.back());
+      if (v_.size() == limit_ + 1) {
+        std::make_heap(v_.begin(), v_.end(), gt_);
+        std::pop_heap(v_.begin(), v_.end(), gt_);
+        state_ = kHeap;
+      }
+    } else if (gt_(e, v_.front())) {
+      v_.back() = e;
+      std::pop_heap(v_.begin(), v_.end(), gt_);
+    }
+  }
+  E peek_bottom() {
+    if (state_ == kUnordered) {
+      size_t m = 0;
+      for (size_t i = 1; i < v_.size(); ++i)
+        if (gt_(v_[m], v_[i])) m = i;
+      if (m != 0) std::swap(v_[0], v_[m]);
+      state_ = kBottomKnown;
+    }
+    return v_.front();
+  }
+  // Destructive, descending order; caller calls reset() afterwards.
+  std::vector<E> extract() {
+    std::vector<E> out;
+    out.swap(v_);
+    if (state_ != kHeap) {
+      std::sort(out.begin(), out.end(), gt_);
+    } else {
+      out.pop_back();
+      std::sort_heap(out.begin(), out.end(), gt_);
+    }
+    return out;
+  }
+  void reset() { v_.clear(); state_ = kUnordered; }
+  typename std::vector<E>::const_iterator ubegin() const { return v_.begin(); }
+  typename std::vector<E>::const_iterator uend() const { return v_.begin() + size(); }
+
+ private:
+  enum { kUnordered, kBottomKnown, kHeap } state_ = kUnordered;
+  std::vector<E> v_;
+  size_t limit_;
+  Greater gt_;
+};
+
+// ---------------------------------------------------------------------------
+// Alignment candidate stores.
+template <class T>
+struct VecCand {             // reference-shaped candidate
+  T prob;
+  std::vector<int> seq;
+};
+template <class T>
+struct VecCandLess {
+  bool operator()(const VecCand<T>& a, const VecCand<T>& b) const { return a.prob < b.prob; }
+};
+
+template <class T>
+struct FaithfulStore {
+  using Queue = std::priority_queue<VecCand<T>, std::vector<VecCand<T>>, VecCandLess<T>>;
+  struct Slots { Queue q[2]; };  // [0] = blank-ending, [1] = label-ending
+  static bool has(const Slots& s, int k) { return !s.q[k].empty(); }
+  static T prob(const Slots& s, int k) { return s.q[k].top().prob; }
+  static void clear(Slots& s) { s.q[0] = Queue(); s.q[1] = Queue(); }
+  // dst gets candidate (base(src,k) + p, base.seq ++ [label])
+  void add(Slots& dst, int to_k, const Slots& src, int from_k, T base_if_none, T p, int label) {
+    std::vector<int> seq;
+    T base;
+    if (!src.q[from_k].empty()) {
+      VecCand<T> c = src.q[from_k].top();   // copies, like GetBlank/GetNBlank
+      base = c.prob;
+      seq = c.seq;
+    } else {
+      base = base_if_none;
+    }
+    std::vector<int> grown(seq);
+    grown.push_back(label);
+    dst.q[to_k].push(VecCand<T>{base + p, grown});
+  }
+  std::vector<int> sequence(const Slots& s, int k) const { return s.q[k].top().seq; }
+  void reset_all() {}
+};
+
+template <class T>
+struct SharedStore {
+  struct Slots { T p[2]; int32_t id[2]; bool ok[2]; Slots() { ok[0] = ok[1] = false; } };
+  std::vector<std::pair<int32_t, int32_t>> arena;  // (label, prev id or -1)
+  static bool has(const Slots& s, int k) { return s.ok[k]; }
+  static T prob(const Slots& s, int k) { return s.p[k]; }
+  static void clear(Slots& s) { s.ok[0] = s.ok[1] = false; }
+  void add(Slots& dst, int to_k, const Slots& src, int from_k, T base_if_none, T p, int label) {
+    T base;
+    int32_t prev;
+    if (src.ok[from_k]) { base = src.p[from_k]; prev = src.id[from_k]; }
+    else { base = base_if_none; prev = -1; }
+    const T np = base + p;
+    // first-pushed maximum == std::priority_queue::top() under a strict '<'
+    if (dst.ok[to_k] && !(np > dst.p[to_k])) return;
+    arena.emplace_back(label, prev);
+    dst.p[to_k] = np;
+    dst.id[to_k] = (int32_t)arena.size() - 1;
+    dst.ok[to_k] = true;
+  }
+  std::vector<int> sequence(const Slots& s, int k) const {
+    std::vector<int> out;
+    for (int32_t i = s.id[k]; i >= 0; i = arena[i].second) out.push_back(arena[i].first);
+    std::reverse(out.begin(), out.end());
+    return out;
+  }
+  void reset_all() { arena.clear(); }
+};
+
+// ---------------------------------------------------------------------------
+// Prefix-trie node (one per distinct label prefix) and the decoder.
+template <class T, class Store>
+struct Node {
+  Node* parent;
+  int label;
+  std::unordered_map<int, Node*> kids;
+  T old_t = LogZero<T>(), old_b = LogZero<T>(), old_l = LogZero<T>();
+  T new_t = LogZero<T>(), new_b = LogZero<T>(), new_l = LogZero<T>();
+  typename Store::Slots old_c, new_c;
+  Node(Node* p, int l) : parent(p), label(l) {}
+  bool active() const { return new_t != LogZero<T>(); }
+  bool fresh() const { return old_t == LogZero<T>(); }
+  void reset_new() { new_t = new_b = new_l = LogZero<T>(); }
+  void reset_old() { old_t = old_b = old_l = LogZero<T>(); }
+};
+
+template <class T, class Store>
+struct NodeGreater {
+  bool operator()(const Node<T, Store>* a, const Node<T, Store>* b) const { return a->new_t > b->new_t; }
+};
+
+template <class T, class Store>
+class Decoder {
+  using N = Node<T, Store>;
+  using Top = BoundedTop<N*, NodeGreater<T, Store>>;
+
+ public:
+  Decoder(int C, int blank_index, int W, int blank_label)
+      : C_(C), blank_(blank_index), W_(W), blank_label_(blank_label), leaves_(W) { reset(); }
+
+  void reset() {
+    leaves_.reset();
+    pool_.clear();
+    store_.reset_all();
+    pool_.emplace_back(new N(nullptr, -1));
+    root_ = pool_.back().get();
+    root_->new_t = T(0);
+    root_->new_b = T(0);
+    leaves_.push(root_);
+  }
+
+  // ctc_ext_beam_search_decoder.h:69-210
+  void step(const T* x) {
+    T mx = x[0];
+    for (int j = 1; j < C_; ++j) mx = std::max(mx, x[j]);
+    T s = T(0);
+    for (int j = 0; j < C_; ++j) s += NumExp(x[j] - mx);
+    s = NumLog(s);
+    const T norm = mx + s;
+
+    std::vector<N*> branches = leaves_.extract();
+    leaves_.reset();
+    for (N* b : branches) {
+      b->old_t = b->new_t; b->old_b = b->new_b; b->old_l = b->new_l;
+      b->old_c = b->new_c;
+      Store::clear(b->new_c);
+    }
+
+    const T pblank = x[blank_] - norm;
+    for (N* b : branches) {
+      if (b->parent != nullptr) {
+        const T p = x[b->label] - norm;
+        N* P = b->parent;
+        if (P->active()) {
+          const bool same = (b->label == P->label);
+          const T prev = same ? P->old_b : P->old_t;
+          b->new_l = LSE(b->new_l, prev) + x[b->label] - norm;
+          cand(b, 1, P, 0, p, b->label);
+          if (!same) cand(b, 1, P, 1, p, b->label);
+          cand(b, 1, b, 1, p, b->label);
+        } else {
+          b->new_l += x[b->label] - norm;
+          cand(b, 1, b, 1, p, b->label);
+        }
+      }
+      b->new_b = b->old_t + x[blank_] - norm;
+      cand(b, 0, b, 0, pblank, blank_label_);
+      cand(b, 0, b, 1, pblank, blank_label_);
+      b->new_t = LSE(b->new_b, b->new_l);
+      leaves_.push(b);
+    }
+
+    for (N* b : branches) {
+      if (!admissible(b->old_t)) continue;
+      for (int l = 0; l < C_; ++l) {
+        if (l == blank_) continue;
+        N* c = child(b, l);
+        if (c->active()) continue;
+        const T p = x[l] - norm;
+        c->new_b = LogZero<T>();
+        if (l == b->label) {
+          c->new_l = x[l] - norm + b->old_b;
+          cand(c, 1, b, 0, p, l);
+        } else {
+          c->new_l = x[l] - norm + b->old_t;
+          cand(c, 1, b, 0, p, l);
+          cand(c, 1, b, 1, p, l);
+        }
+        c->new_t = c->new_l;
+        if (admissible(c->new_t)) {
+          if (leaves_.size() == (size_t)W_) {
+            N* bottom = leaves_.peek_bottom();
+            bottom->reset_new();
+            Store::clear(bottom->new_c);
+          }
+          leaves_.push(c);
+        } else {
+          c->reset_old();
+          c->reset_new();
+          Store::clear(c->old_c);
+          Store::clear(c->new_c);
+        }
+      }
+    }
+  }
+
+  // ctc_ext_beam_search_decoder.h:230-261.  Returns 0, 1 (n > W) or 2 (n > leaves).
+  int top_paths(int n, bool merge, std::vector<std::vector<int>>& paths,
+                std::vector<std::vector<int>>& aligns, std::vector<T>& lps, int& no_label_events) {
+    paths.clear(); aligns.clear(); lps.clear();
+    if (n > W_) return 1;
+    if ((size_t)n > leaves_.size()) return 2;
+    Top best(n);
+    for (auto it = leaves_.ubegin(); it != leaves_.uend(); ++it) best.push(*it);
+    std::vector<N*> sel = best.extract();
+    for (int i = 0; i < n; ++i) {
+      N* e = sel[i];
+      aligns.push_back(alignment(e, no_label_events));
+      std::vector<int> labels;
+      int prev = -1;
+      for (const N* c = e; c->parent != nullptr; c = c->parent) {
+        if (!merge || c->label != prev) labels.push_back(c->label);
+        prev = c->label;
+      }
+      std::reverse(labels.begin(), labels.end());
+      paths.push_back(labels);
+      lps.push_back(e->new_t);
+    }
+    return 0;
+  }
+
+ private:
+  bool admissible(T total) {
+    return total > LogZero<T>() &&
+           (leaves_.size() < (size_t)W_ || total > leaves_.peek_bottom()->new_t);
+  }
+  N* child(N* b, int l) {
+    auto it = b->kids.find(l);
+    if (it != b->kids.end()) return it->second;
+    pool_.emplace_back(new N(b, l));
+    b->kids.emplace(l, pool_.back().get());
+    return pool_.back().get();
+  }
+  // ctc_beam_entry.h:190-228: receiver r gets a candidate built on
+  // src's previous-step candidate of kind from_k (0 = blank-ending).
+  void cand(N* r, int to_k, const N* src, int from_k, T p, int label) {
+    T base_if_none = LogZero<T>();
+    if (r->parent == nullptr || (r->parent->parent == nullptr && r->fresh()))
+      base_if_none = (from_k == 0) ? T(0) : LogZero<T>();
+    store_.add(r->new_c, to_k, src->old_c, from_k, base_if_none, p, label);
+  }
+  std::vector<int> alignment(N* e, int& no_label_events) {
+    const bool hb = Store::has(e->new_c, 0), hn = Store::has(e->new_c, 1);
+    if (hb && hn) return store_.sequence(e->new_c, Store::prob(e->new_c, 0) > Store::prob(e->new_c, 1) ? 0 : 1);
+    if (hb) return store_.sequence(e->new_c, 0);
+    if (hn) return store_.sequence(e->new_c, 1);
+    ++no_label_events;   // reference prints "No label seq available"
+    return {};
+  }
+
+  int C_, blank_, W_, blank_label_;
+  Top leaves_;
+  std::vector<std::unique_ptr<N>> pool_;
+  N* root_ = nullptr;
+  Store store_;
+};
+
+}  // namespace oracle
+
+// ---------------------------------------------------------------------------
+// C ABI used by oracle/oracle.py (ctypes).  Mirrors the Compute() batch
+// driver (kernels.cc:20-95): items decoded one after another with one decoder
+// that is reset between items; the first failing item aborts the call.
+struct OracleResult {
+  int32_t status;          // 0 ok; 1 "requested more paths than the beam width."
+                           //      2 "Less leaves in the beam search than requested."
+  int32_t no_label_events;
+  int64_t total_dec, total_ali;
+  int64_t* dec_len;        // [B*P]   (b-major)
+  int64_t* ali_len;        // [B*P]
+  int32_t* dec_vals;       // concatenation over (b, p) in b-major order
+  int32_t* ali_vals;
+  double* log_prob;        // [B*P]
+};
+
+template <class T, class Store>
+static OracleResult* run(const T* x, const int32_t* seq_len, int64_t Tmax, int64_t B, int64_t C,
+                         int W, int P, int merge, int blank_index, int blank_label) {
+  OracleResult* r = new OracleResult();
+  memset(r, 0, sizeof(*r));
+  std::vector<std::vector<int>> dec_all, ali_all;
+  std::vector<double> lp(B * P, 0.0);
+  oracle::Decoder<T, Store> dec((int)C, blank_index, W, blank_label);
+  std::vector<T> row(C);
+  for (int64_t b = 0; b < B; ++b) {
+    for (int64_t t = 0; t < seq_len[b]; ++t) {
+      memcpy(row.data(), x + (t * B + b) * C, sizeof(T) * C);
+      dec.step(row.data());
+    }
+    std::vector<std::vector<int>> paths, aligns;
+    std::vector<T> lps;
+    int st = dec.top_paths(P, merge != 0, paths, aligns, lps, r->no_label_events);
+    if (st != 0) { r->status = st; return r; }
+    dec.reset();
+    for (int p = 0; p < P; ++p) {
+      lp[b * P + p] = (double)lps[p];
+      dec_all.push_back(paths[p]);
+      ali_all.push_back(aligns[p]);
+    }
+  }
+  r->dec_len = new int64_t[B * P + 1];
+  r->ali_len = new int64_t[B * P + 1];
+  r->log_prob = new double[B * P + 1];
+  for (int64_t i = 0; i < B * P; ++i) {
+    r->dec_len[i] = (int64_t)dec_all[i].size();
+    r->ali_len[i] = (int64_t)ali_all[i].size();
+    r->total_dec += r->dec_len[i];
+    r->total_ali += r->ali_len[i];
+    r->log_prob[i] = lp[i];
+  }
+  r->dec_vals = new int32_t[r->total_dec + 1];
+  r->ali_vals = new int32_t[r->total_ali + 1];
+  int64_t od = 0, oa = 0;
+  for (int64_t i = 0; i < B * P; ++i) {
+    for (int v : dec_all[i]) r->dec_vals[od++] = v;
+    for (int v : ali_all[i]) r->ali_vals[oa++] = v;
+  }
+  return r;
+}
+
+extern "C" {
+
+// dtype 0 = float32, 1 = float64; mode 0 = faithful store, 1 = shared store.
+OracleResult* oracle_decode(int dtype, int mode, const void* x, const int32_t* seq_len,
+                            int64_t T, int64_t B, int64_t C, int W, int P, int merge,
+                            int blank_index, int blank_label) {
+  if (dtype == 0) {
+    const float* xf = (const float*)x;
+    return mode == 0 ? run<float, oracle::FaithfulStore<float>>(xf, seq_len, T, B, C, W, P, merge, blank_index, blank_label)
+                     : run<float, oracle::SharedStore<float>>(xf, seq_len, T, B, C, W, P, merge, blank_index, blank_label);
+  }
+  const double* xd = (const double*)x;
+  return mode == 0 ? run<double, oracle::FaithfulStore<double>>(xd, seq_len, T, B, C, W, P, merge, blank_index, blank_label)
+                   : run<double, oracle::SharedStore<double>>(xd, seq_len, T, B, C, W, P, merge, blank_index, blank_label);
+}
+
+void oracle_free(OracleResult* r) {
+  if (!r) return;
+  delete[] r->dec_len; delete[] r->ali_len; delete[] r->dec_vals; delete[] r->ali_vals;
+  delete[] r->log_prob;
+  delete r;
+}
+
+}  // extern "C"

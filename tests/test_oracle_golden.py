@@ -1,0 +1,69 @@
+"""Pins the CPU oracle (test infrastructure) to the reference's only golden
+vector: python/ops/ctc_ext_beam_search_decoder_ops_test.py:20-100."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "paper_example.json")))
+
+
+def _check(out):
+    a = GOLD["attrs"]
+    for p in range(a["top_paths"]):
+        np.testing.assert_array_equal(out.decoded_indices[p], np.asarray(GOLD["decoded_indices"][p]))
+        np.testing.assert_array_equal(out.decoded_values[p], np.asarray(GOLD["decoded_values"][p]))
+        np.testing.assert_array_equal(out.decoded_shape[p], np.asarray(GOLD["decoded_shape"][p]))
+        np.testing.assert_array_equal(out.alignment_indices[p], np.asarray(GOLD["alignment_indices"][p]))
+        np.testing.assert_array_equal(out.alignment_values[p], np.asarray(GOLD["alignment_values"][p]))
+        np.testing.assert_array_equal(out.alignment_shape[p], np.asarray(GOLD["alignment_shape"][p]))
+    # the reference test's assertAllClose defaults
+    np.testing.assert_allclose(out.log_probability, np.asarray(GOLD["log_probability"]), rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("mode", ["faithful", "shared"])
+def test_oracle_reproduces_paper_golden(dtype, mode):
+    a = GOLD["attrs"]
+    logits = np.log(np.asarray(GOLD["probs"])).astype(dtype)
+    out = oracle.decode(logits, GOLD["sequence_length"], a["beam_width"], a["top_paths"],
+                        a["merge_repeated"], a["blank_index"], a["blank_label"], mode=mode)
+    _check(out)
+
+
+def test_oracle_modes_agree_random():
+    rng = np.random.default_rng(7)
+    for _ in range(40):
+        T, B, C = rng.integers(1, 30), rng.integers(1, 4), rng.integers(2, 9)
+        W = int(rng.integers(1, 12))
+        P = int(rng.integers(1, W + 1))
+        x = rng.standard_normal((T, B, C)).astype(np.float32)
+        if rng.random() < 0.3:
+            x = np.round(x * 2) / 2   # tie-heavy
+        sl = rng.integers(T // 2, T + 1, size=B).astype(np.int32)
+        kw = dict(merge_repeated=bool(rng.integers(2)), blank_index=int(rng.integers(C)),
+                  blank_label=int(rng.integers(-1, C)))
+        try:
+            a = oracle.raw_decode(x, sl, W, P, mode="faithful", **kw)
+        except oracle.OracleError as e:
+            with pytest.raises(oracle.OracleError, match=str(e).split('.')[0]):
+                oracle.raw_decode(x, sl, W, P, mode="shared", **kw)
+            continue
+        b = oracle.raw_decode(x, sl, W, P, mode="shared", **kw)
+        assert a[0] == b[0] and a[1] == b[1]
+        np.testing.assert_array_equal(a[2], b[2])
+
+
+def test_oracle_errors():
+    x = np.zeros((4, 1, 3), np.float32)
+    with pytest.raises(oracle.OracleError, match="requested more paths than the beam width."):
+        oracle.decode(x, [4], 2, 3)
+    with pytest.raises(oracle.OracleError, match="Less leaves in the beam search than requested."):
+        oracle.decode(x[:1], [1], 10, 5)
+    with pytest.raises(oracle.OracleError, match="max_time is 0"):
+        oracle.decode(np.zeros((0, 1, 3), np.float32), [0], 2, 1)
+    with pytest.raises(oracle.OracleError, match=r"sequence_length\(0\) <= 4"):
+        oracle.decode(x, [5], 2, 1)
