@@ -1,0 +1,192 @@
+"""bench.py — decoded frames/s of the MI355X CTC ext beam search decoder.
+
+Workload (BASELINE.json metric, configs[2] = "cfg3"): per GPU a batch of
+B=256 items, T=1500 frames, C=29 classes, beam_width=128, top_paths=3,
+merge_repeated=True; float32 logits [T,B,C] ~ N(0,1) from
+numpy.random.default_rng(20251015) (rank r>0: seed 20251015+r), already in
+HBM when the timed region starts.  One step = one full decode call through the
+C ABI (row normaliser, beam decode, traceback, int64 SparseTensor components
+materialised in HBM) plus, for N>1, the RCCL gather of every rank's outputs to
+rank 0.  Weak scaling: the global batch is 256*N.
+
+Prints ONE JSON line on rank 0 (see the contract in the task statement), with
+a roofline object for the dominant kernel (ctcx_beam_decode, timed with HIP
+events on the stream it runs on) and a cpu_baseline object (the oracle's
+reference-cost mode on a bounded sample, N=1 only).
+"""
+import argparse
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ctc-beam-search-op_amd"))
+
+CONFIGS = {
+    # name: (B per GPU, T, C, beam_width, top_paths, merge_repeated, blank_index)
+    "cfg1": (2, 50, 6, 4, 1, False, 0),
+    "cfg2": (32, 1000, 29, 64, 1, False, 0),
+    "cfg3": (256, 1500, 29, 128, 3, True, 0),
+    "cfg4": (128, 2000, 1000, 64, 1, False, 0),      # 1024 over 8 GPUs
+    "cfg5": (512, 3000, 5000, 256, 1, False, 0),
+}
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def make_inputs(cfg, rank):
+    B, T, C = cfg[0], cfg[1], cfg[2]
+    rng = np.random.default_rng(20251015 + rank)
+    x = rng.standard_normal((T, B, C), dtype=np.float32)
+    sl = np.full(B, T, dtype=np.int32)
+    return x, sl
+
+
+def algorithmic_bytes(sl, C, P, out, tsize=4):
+    """logits read + seq_len + int64 SparseTensor components +
+    shapes + log_prob, from the actual output sizes."""
+    n = sum(int(out.decoded_values[p].numel()) + int(out.alignment_values[p].numel()) for p in range(P))
+    B = len(sl)
+    return int(np.sum(sl, dtype=np.int64)) * C * tsize + 4 * B + 24 * n + 32 * P + B * P * tsize
+
+
+def _cpu_worker(args):
+    x, sl, W, P, merge, blank = args
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    t0 = time.perf_counter()
+    oracle.raw_decode(x, sl, W, P, merge, blank, -1, mode="faithful")
+    return time.perf_counter() - t0
+
+
+def cpu_baseline(cfg, n_workers, t_cap):
+    """The oracle in reference-cost mode (per-candidate std::vector alignment
+    copies, per-child heap nodes, TopN heap) on `n_workers` items of the
+    workload, one item per process — the reference op is single-threaded
+    (kernels.cc:68), so one process per core is its all-cores form."""
+    B, T, C, W, P, merge, blank = cfg
+    T = min(T, t_cap)
+    rng = np.random.default_rng(20251015)
+    jobs = []
+    for _ in range(n_workers):
+        x = rng.standard_normal((T, 1, C), dtype=np.float32)
+        jobs.append((x, np.array([T], np.int32), W, P, merge, blank))
+    ctx = mp.get_context("spawn")
+    t0 = time.perf_counter()
+    with ctx.Pool(n_workers) as pool:
+        per_item = pool.map(_cpu_worker, jobs)
+    wall = time.perf_counter() - t0
+    frames = n_workers * T
+    return {"value": frames / wall, "unit": "frames/s", "cores": n_workers, "kind": "port",
+            "sample": "%d items x T=%d of the workload shape (C=%d, beam_width=%d, top_paths=%d, "
+                      "merge_repeated=%s), oracle reference-cost mode, one item per process"
+                      % (n_workers, T, C, W, P, merge),
+            "per_core_value": T / float(np.mean(per_item)), "wall_s": wall}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-workers", type=int, default=int(os.environ.get("CTCX_CPU_WORKERS", "16")))
+    ap.add_argument("--cpu-tcap", type=int, default=1500)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-gather", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import ctcext_amd
+    from ctcext_amd import _lib
+    from ctcext_amd.sharded import gather_to_root
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    cfg = CONFIGS[args.config]
+    B, T, C, W, P, merge, blank = cfg
+    x_np, sl_np = make_inputs(cfg, rank)
+    x = torch.as_tensor(x_np, device=dev)
+    sl = torch.as_tensor(sl_np, device=dev)
+    torch.cuda.synchronize()
+
+    flags = _lib.CTCEXT_FLAG_PROFILE
+    dec = ctcext_amd.get_decoder(local)
+
+    def step():
+        out = ctcext_amd.ctc_ext_beam_search_decoder(x, sl, W, P, merge_repeated=merge,
+                                                     blank_index=blank, blank_label=-1, flags=flags)
+        if world > 1 and not args.no_gather:
+            gather_to_root(out, rank * B, P)
+        return out
+
+    for _ in range(args.warmup):
+        out = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kms, lit = [], 0
+    for _ in range(args.steps):
+        out = step()
+        st = dec.last_stats
+        kms.append(st["decode_kernel_ms"])
+        lit += st["literal_frames"]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    frames_per_step = int(sl_np.sum()) * world
+    value = frames_per_step * args.steps / elapsed
+    ms = 1e3 * elapsed / args.steps
+    kavg = float(np.mean(kms))
+    abytes = algorithmic_bytes(sl_np, C, P, out)
+    achieved = abytes / (kavg * 1e-3) / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
+    if os.path.exists(pmc):
+        traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+    res = {
+        "metric": "decoded frames/sec at B=256, T=1500, C=29, beam_width=128; 1/2/4/8 GPUs",
+        "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": args.config, "global_batch": B * world, "batch_per_gpu": B,
+                   "seq_len": T, "num_classes": C, "beam_width": W, "top_paths": P,
+                   "merge_repeated": merge, "parallelism": "batch-shard x%d" % world,
+                   "gather": world > 1 and not args.no_gather},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "ctcx_beam_decode", "kernel_ms": kavg,
+                     "algorithmic_bytes_per_launch": abytes},
+        "literal_frames_per_step": lit / max(args.steps, 1),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_workers, args.cpu_tcap)
+        res["cpu_baseline"]["gpu_over_cpu"] = value / res["cpu_baseline"]["value"]
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

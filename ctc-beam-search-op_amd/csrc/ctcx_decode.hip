@@ -1,0 +1,852 @@
+// ctcx_decode.hip — MI355X (gfx950) kernels for CTC beam search with per-beam
+// best-alignment tracking.  Drop-in replacement for the reference CPU path
+//   CTCExtBeamSearchDecoderOp<T>::Compute   (kernels/..._kernels.cc:20-95)
+//   CTCExtBeamSearchDecoder<T>::Step/TopPaths (util/ctc_ext_beam_search_decoder.h:66-261)
+//   BeamEntry / TopN / LogSumExp             (util/ctc_beam_entry.h, util/ctc_loss_util.h)
+//
+// Kernels (launch order; DESIGN.md has the roofline of each):
+//   ctcx_row_norm     one thread per (t, b) row: softmax normaliser, sequential
+//                     glibc-exact expf sum (decoder.h:72-80).
+//   ctcx_beam_decode  one wave64 workgroup per batch item, persistent over t.
+//                     Beam state lives in LDS; per frame it writes one 16-byte
+//                     record per surviving beam (prefix back-link + alignment
+//                     backpointers) to HBM.
+//   ctcx_traceback    one thread per (item, path, {decoded, alignment}): walks
+//                     the records backwards (LabelSeq / AlignmentLabelSeq).
+//   ctcx_scan         per (path, kind) exclusive scan of sequence lengths.
+//   ctcx_pack         int64 SparseTensor components (StoreAllDecodedSequences).
+//
+// The beam update per frame has two exact implementations:
+//   * the FAST path: slot model — beams sit at fixed LDS slots, their totals in
+//     registers; the streaming top-W is a sequence of (evict the unique minimum,
+//     insert) events found by wave ballots; final order by a rank sort.  Exact
+//     whenever no two live totals are equal at an eviction or in the final
+//     order and every total is finite (checked each frame).
+//   * the LITERAL path (one lane): the reference's own TopN state machine and
+//     libstdc++ heap/introsort layout over slot ids (ctcx_topn.h).  A frame
+//     whose fast path hits a tie or a non-finite total is replayed here from
+//     the untouched frame-start state, so tie order matches the reference.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ctcx_kernels.h"
+#include "ctcx_topn.h"
+#include "glibc_math.h"
+
+namespace ctcx {
+
+// branch / entry flag bits
+constexpr int F_ROOT = 1;    // this node is the root (empty prefix)
+constexpr int F_PROOT = 2;   // this node's parent is the root
+constexpr int F_HB = 4;      // has a blank-ending alignment candidate
+constexpr int F_HN = 8;      // has a label-ending alignment candidate
+// per-frame branch state bits
+constexpr int S_EVICT = 1;   // pushed this frame, then evicted from the beam
+constexpr int S_DEACT = 2;   // deactivated (oldp reset): grows no children
+
+template <typename T> __host__ __device__ __forceinline__ T ninf();
+template <> __host__ __device__ __forceinline__ float ninf<float>() { return -__builtin_inff(); }
+template <> __host__ __device__ __forceinline__ double ninf<double>() { return -__builtin_inf(); }
+template <typename T> __host__ __device__ __forceinline__ T pinf();
+template <> __host__ __device__ __forceinline__ float pinf<float>() { return __builtin_inff(); }
+template <> __host__ __device__ __forceinline__ double pinf<double>() { return __builtin_inf(); }
+
+// util/ctc_loss_util.h:29-41 — float libm (expf, log1pf) even for T=double.
+template <typename T>
+__host__ __device__ __forceinline__ T lse(T a, T b) {
+  if (a == ninf<T>()) return b;
+  if (b == ninf<T>()) return a;
+  return (a > b) ? a + (T)gm::log1pf(gm::expf((float)(b - a)))
+                 : b + (T)gm::log1pf(gm::expf((float)(a - b)));
+}
+
+__device__ __forceinline__ float bcast(float v, int k) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), k));
+}
+__device__ __forceinline__ double bcast(double v, int k) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, k);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), k);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ int bcast(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
+
+template <typename T>
+__device__ __forceinline__ T wave_min(T v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const T w = __shfl_xor(v, o);
+    v = (w < v) ? w : v;
+  }
+  return v;
+}
+
+// "first-pushed maximum" of a std::priority_queue with a strict '<' comparer
+// (ctc_beam_entry.h:65-73): only a strictly greater push replaces the top.
+template <typename T>
+struct Best {
+  T p;
+  uint32_t bp;
+  bool ok;
+  __host__ __device__ __forceinline__ void push(T prob, uint32_t b) {
+    if (!ok || prob > p) { p = prob; bp = b; ok = true; }
+  }
+};
+
+template <typename T>
+struct Ctx {
+  // branch arrays, double-buffered by frame parity: [buf][i]
+  T* ot[2]; T* ob[2]; T* ol[2]; T* cb[2]; T* cn[2];
+  int* lab[2]; int* par[2]; int* flg[2];
+  int* head; int* sib; int* bst; int* newpos;
+  // entries (fast: beam slots; literal: node slots), capacity 2W+2
+  T* et; T* eb; T* el; T* ecb; T* ecn;
+  uint32_t* ebpb; uint32_t* ebpn; uint32_t* ekind; int* elab; int* eflg;
+  int* heap; int* tops; int* freel; int* sorted;
+  T* row;
+  int* misc;
+  // prefix identity: 128-bit hash of each branch's label prefix and of its
+  // parent's, [buf][i]; htab maps the hash of a frame's new leaves to position
+  uint64_t* ha[2]; uint64_t* hb[2]; uint64_t* pha[2]; uint64_t* phb[2];
+  int* htab;
+  int W, C, blank, enc, hts;
+};
+
+// Prefix hashing (stands in for the reference's trie, ctc_beam_entry.h:114-122
+// and 248-269): a node's identity is its label prefix; h(prefix + [l]) =
+// mix(h(prefix), l), two independent 64-bit chains.  For a fixed label each
+// chain step is a bijection, so siblings and same-label children of distinct
+// parents never collide; an accidental collision needs 2^-128 luck.
+__host__ __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
+  k ^= k >> 33; k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+__host__ __device__ __forceinline__ void hmix(uint64_t a, uint64_t b, int l, uint64_t& oa, uint64_t& ob) {
+  const uint64_t x = (uint64_t)(uint32_t)l + 1ull;
+  oa = fmix64(a ^ (x * 0x9E3779B97F4A7C15ull));
+  ob = fmix64(b + x * 0xD6E8FEB86659FD93ull + 0x632BE59BD9B4E019ull);
+}
+constexpr uint64_t kRootHa = 0x243F6A8885A308D3ull, kRootHb = 0x13198A2E03707344ull;
+
+template <typename T>
+__host__ __device__ void carve(Ctx<T>& cx, char* base, int W, int C) {
+  const size_t ENC = 2 * (size_t)W + 2;
+  auto a16 = [](size_t v) { return (v + 15) & ~(size_t)15; };
+  char* p = base;
+  for (int b = 0; b < 2; ++b) {
+    T* q = (T*)p;
+    cx.ot[b] = q; cx.ob[b] = q + W; cx.ol[b] = q + 2 * W; cx.cb[b] = q + 3 * W; cx.cn[b] = q + 4 * W;
+    p += a16(5 * (size_t)W * sizeof(T));
+  }
+  for (int b = 0; b < 2; ++b) {
+    int* q = (int*)p;
+    cx.lab[b] = q; cx.par[b] = q + W; cx.flg[b] = q + 2 * W;
+    p += a16(3 * (size_t)W * 4);
+  }
+  {
+    int* q = (int*)p;
+    cx.head = q; cx.sib = q + W; cx.bst = q + 2 * W; cx.newpos = q + 3 * W;
+    p += a16(4 * (size_t)W * 4);
+  }
+  {
+    T* q = (T*)p;
+    cx.et = q; cx.eb = q + ENC; cx.el = q + 2 * ENC; cx.ecb = q + 3 * ENC; cx.ecn = q + 4 * ENC;
+    p += a16(5 * ENC * sizeof(T));
+  }
+  {
+    uint32_t* q = (uint32_t*)p;
+    cx.ebpb = q; cx.ebpn = q + ENC; cx.ekind = q + 2 * ENC;
+    cx.elab = (int*)(q + 3 * ENC); cx.eflg = (int*)(q + 4 * ENC);
+    p += a16(5 * ENC * 4);
+  }
+  cx.heap = (int*)p; p += a16(((size_t)W + 1) * 4);
+  cx.tops = (int*)p; p += a16(((size_t)W + 1) * 4);
+  cx.freel = (int*)p; p += a16(ENC * 4);
+  cx.sorted = (int*)p; p += a16((size_t)W * 4);
+  cx.row = (T*)p; p += a16((size_t)C * sizeof(T));
+  cx.misc = (int*)p; p += 64;
+  for (int b = 0; b < 2; ++b) {
+    uint64_t* q = (uint64_t*)p;
+    cx.ha[b] = q; cx.hb[b] = q + W; cx.pha[b] = q + 2 * W; cx.phb[b] = q + 3 * W;
+    p += 4 * (size_t)W * 8;
+  }
+  cx.hts = htab_size(W);
+  cx.htab = (int*)p;
+  cx.W = W; cx.C = C; cx.enc = (int)ENC;
+}
+
+// Alignment candidate "from S.kind" for a receiver (ctc_beam_entry.h:190-228).
+// restart: the base probability when S has no candidate of that kind.
+template <typename T>
+__host__ __device__ __forceinline__ void cand_from(const Ctx<T>& cx, int buf, int src, int kind, T p, T restart,
+                                          Best<T>& best) {
+  const int f = cx.flg[buf][src];
+  const bool has = (f & (kind == 0 ? F_HB : F_HN)) != 0;
+  const T base = has ? (kind == 0 ? cx.cb[buf][src] : cx.cn[buf][src]) : restart;
+  best.push(base + p, has ? (((uint32_t)src << 1) | (uint32_t)kind) : kBpRestart);
+}
+
+// Recursion for branch i (decoder.h:95-143).  Reads the frame-start branch
+// arrays and the entry i's current newp (rolled = oldp, except in literal mode
+// where a parent processed earlier may have changed its own entry).
+template <typename T>
+__host__ __device__ void recurse_branch(const Ctx<T>& cx, int buf, int i, T norm, bool literal) {
+  const T NI = ninf<T>();
+  const int f = cx.flg[buf][i];
+  const int L = cx.lab[buf][i];
+  const bool isroot = (f & F_ROOT) != 0;
+  const T o_t = cx.ot[buf][i];
+  const bool fresh = (o_t == NI);
+  // restart base for a from-blank candidate with receiver i
+  const T rs_blank = (isroot || ((f & F_PROOT) && fresh)) ? T(0) : NI;
+  T nl = cx.el[i];
+  Best<T> bn{T(0), kBpNone, false}, bb{T(0), kBpNone, false};
+  if (!isroot) {
+    const T xl = cx.row[L];
+    const T p = xl - norm;
+    const int P = cx.par[buf][i];
+    const bool pactive = (P >= 0) && (!literal || cx.et[P] != NI);
+    if (pactive) {
+      const bool same = (L == cx.lab[buf][P]);
+      const T prev = same ? cx.ob[buf][P] : cx.ot[buf][P];
+      nl = lse(nl, prev) + xl - norm;
+      cand_from(cx, buf, P, 0, p, rs_blank, bn);
+      if (!same) cand_from(cx, buf, P, 1, p, NI, bn);
+      cand_from(cx, buf, i, 1, p, NI, bn);
+    } else {
+      nl += xl - norm;
+      cand_from(cx, buf, i, 1, p, NI, bn);
+    }
+  }
+  const T xb = cx.row[cx.blank];
+  const T nbk = o_t + xb - norm;
+  const T pb = xb - norm;
+  // existing new candidates (literal replay of a duplicate visit) are kept
+  const int ef = cx.eflg[i];
+  if (ef & F_HB) { bb.ok = true; bb.p = cx.ecb[i]; bb.bp = cx.ebpb[i]; }
+  if (ef & F_HN) {
+    Best<T> prior{cx.ecn[i], cx.ebpn[i], true};
+    if (bn.ok) prior.push(bn.p, bn.bp);
+    bn = prior;
+  }
+  cand_from(cx, buf, i, 0, pb, rs_blank, bb);
+  cand_from(cx, buf, i, 1, pb, NI, bb);
+  cx.eb[i] = nbk;
+  cx.el[i] = nl;
+  cx.et[i] = lse(nbk, nl);
+  cx.ecb[i] = bb.p; cx.ebpb[i] = bb.bp;
+  cx.ecn[i] = bn.p; cx.ebpn[i] = bn.bp;
+  cx.eflg[i] = (bb.ok ? F_HB : 0) | (bn.ok ? F_HN : 0);
+  cx.ekind[i] = ((uint32_t)i << 1);
+  cx.elab[i] = L;
+}
+
+// ---------------------------------------------------------------------------
+// FAST path for one frame (whole wave).  Returns false if the frame must be
+// replayed literally.  On success cx.sorted[0..*n_out) holds the surviving
+// entry slots in descending total order.
+template <typename T, int R>
+__device__ bool fast_step(Ctx<T>& cx, int buf, int nb, T norm, int* n_out) {
+  const int lane = threadIdx.x;
+  const T NI = ninf<T>();
+  const int W = cx.W;
+  const int C = cx.C;
+  const int blank = cx.blank;
+
+  // roll + recursion, lanes over branches
+  for (int r = 0; r < R; ++r) {
+    const int i = r * 64 + lane;
+    if (i < nb) {
+      cx.et[i] = cx.ot[buf][i]; cx.eb[i] = cx.ob[buf][i]; cx.el[i] = cx.ol[buf][i];
+      cx.eflg[i] = 0;
+      cx.bst[i] = 0;
+    }
+  }
+  __syncthreads();
+  for (int r = 0; r < R; ++r) {
+    const int i = r * 64 + lane;
+    if (i < nb) recurse_branch(cx, buf, i, norm, false);
+  }
+  __syncthreads();
+
+  T val[R];
+  bool finite = true;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int e = r * 64 + lane;
+    val[r] = (e < nb) ? cx.et[e] : pinf<T>();
+    if (e < nb && !(val[r] > NI && val[r] < pinf<T>())) finite = false;
+  }
+  if (__ballot(!finite)) return false;
+
+  int size = nb;
+  bool full = (size >= W);
+  T bottom = NI;
+  if (full) {
+    T m = val[0];
+#pragma unroll
+    for (int r = 1; r < R; ++r) m = (val[r] < m) ? val[r] : m;
+    bottom = wave_min(m);
+  }
+
+  // grow: offers in (branch order, label order), 64 per chunk
+  const int Cm1 = C - 1;
+  const int64_t total = (int64_t)nb * Cm1;
+  for (int64_t f0 = 0; f0 < total; f0 += 64) {
+    const int i0 = (int)(f0 / Cm1);
+    if (full && !(cx.ot[buf][i0] > bottom)) break;   // every later branch is skipped
+    const int64_t f = f0 + lane;
+    const bool valid = f < total;
+    const int i = valid ? (int)(f / Cm1) : i0;
+    const int li = valid ? (int)(f - (int64_t)i * Cm1) : 0;
+    const int l = li + (li >= blank ? 1 : 0);
+    const int bl = cx.lab[buf][i];
+    const int bflg = cx.flg[buf][i];
+    const T bt = cx.ot[buf][i];
+    bool live = valid && !(cx.bst[i] & S_DEACT);
+    const T xl = cx.row[l];
+    const T p = xl - norm;
+    const T s = p + ((l == bl) ? cx.ob[buf][i] : bt);
+    int c = -1;
+    if (live) {
+      for (int k = cx.head[i]; k >= 0; k = cx.sib[k])
+        if (cx.lab[buf][k] == l) { c = k; break; }
+    }
+    const bool isbc = c >= 0;
+    bool cev = isbc && (cx.bst[c] & S_EVICT);
+    // label-ending candidate for the child (decoder.h:172-185)
+    const bool recv_fresh = isbc ? (cx.ot[buf][c] == NI) : true;
+    const T rs_blank = ((bflg & F_ROOT) && recv_fresh) ? T(0) : NI;
+    Best<T> cd{T(0), kBpNone, false};
+    cand_from(cx, buf, i, 0, p, rs_blank, cd);
+    if (l != bl) cand_from(cx, buf, i, 1, p, NI, cd);
+
+    uint64_t done = 0;
+    while (true) {
+      const bool want = live && (isbc ? cev : (s > (full ? bottom : NI)));
+      const uint64_t m = __ballot(want) & ~done;
+      if (m == 0) break;
+      const int k = __ffsll((unsigned long long)m) - 1;
+      done = (k == 63) ? ~0ull : ((2ull << k) - 1ull);
+      const int k_isbc = bcast((int)isbc, k);
+      const int k_c = bcast(c, k);
+      const T k_s = bcast(s, k);
+      const bool accept = k_isbc ? (k_s > NI && (!full || k_s > bottom)) : true;
+      if (accept) {
+        int pos;
+        if (!full) {
+          pos = size++;
+        } else {
+          // the unique minimum is evicted; a tie at the minimum is layout-dependent
+          int cnt = 0;
+          pos = -1;
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const uint64_t mm = __ballot(val[r] == bottom);
+            cnt += __popcll(mm);
+            if (pos < 0 && mm) pos = r * 64 + __ffsll((unsigned long long)mm) - 1;
+          }
+          if (cnt != 1) return false;
+          const uint32_t kd = cx.ekind[pos];
+          if (!(kd & 1u)) {
+            const int j = (int)(kd >> 1);
+            if (lane == 0) cx.bst[j] |= S_EVICT;
+            if (isbc && c == j) cev = true;
+          }
+        }
+        if (lane == k) {
+          cx.et[pos] = s; cx.eb[pos] = NI; cx.el[pos] = s;
+          cx.ecn[pos] = cd.p; cx.ebpn[pos] = cd.bp;
+          cx.eflg[pos] = F_HN;
+          cx.ekind[pos] = isbc ? ((uint32_t)c << 1) : (((uint32_t)i << 1) | 1u);
+          cx.elab[pos] = l;
+          if (isbc) cx.bst[c] &= ~S_EVICT;
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          if (r * 64 + lane == pos) val[r] = k_s;
+        if (!full && size == W) full = true;
+        if (full) {
+          T mv = val[0];
+#pragma unroll
+          for (int r = 1; r < R; ++r) mv = (val[r] < mv) ? val[r] : mv;
+          bottom = wave_min(mv);
+        }
+      } else {
+        // re-offered evicted branch rejected -> deactivated (decoder.h:200-205)
+        if (lane == 0) cx.bst[k_c] |= S_DEACT;
+        if (i == k_c) live = false;
+      }
+      __syncthreads();
+    }
+  }
+
+  // final order: rank sort, descending; any equal totals -> literal replay
+  const int n = size;
+  bool tie = false;
+  for (int r = 0; r < R; ++r) {
+    const int e = r * 64 + lane;
+    if (e < n) {
+      const T v = val[r];
+      int rank = 0;
+      for (int q = 0; q < n; ++q) {
+        const T w = cx.et[q];
+        rank += (w > v) ? 1 : 0;
+        tie |= (q != e) && (w == v);
+      }
+      cx.sorted[rank] = e;
+    }
+  }
+  if (__ballot(tie)) return false;
+  __syncthreads();
+  *n_out = n;
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// LITERAL path for one frame, executed by lane 0 (decoder.h:69-210 verbatim in
+// semantics, including TopN layout).  Returns the number of surviving entries
+// (sorted slots in cx.sorted); for the last frame also fills cx.tops[0..P)
+// with the TopPaths selection as slots.  *err = 1 on a duplicate-beam state.
+template <typename T>
+__host__ __device__ int literal_step(Ctx<T>& cx, int buf, int nb, T norm, bool last, int P, int* err,
+                            int* n_leaves) {
+  const T NI = ninf<T>();
+  const int W = cx.W, C = cx.C, blank = cx.blank;
+  for (int i = 0; i < nb; ++i) {
+    cx.et[i] = cx.ot[buf][i]; cx.eb[i] = cx.ob[buf][i]; cx.el[i] = cx.ol[buf][i];
+    cx.eflg[i] = 0;
+    cx.bst[i] = 0;
+  }
+  int nfree = 0;
+  for (int s = cx.enc - 1; s >= nb; --s) cx.freel[nfree++] = s;
+  SlotGreater<T> gt{cx.et};
+  LitTop h{cx.heap, 0, W, kTopUnordered};
+
+  for (int i = 0; i < nb; ++i) {
+    recurse_branch(cx, buf, i, norm, true);
+    lit_top_push(h, i, gt);
+  }
+
+  for (int i = 0; i < nb; ++i) {
+    {
+      const T bt = cx.ot[buf][i];
+      if (!(bt > NI && (h.size() < W || bt > cx.et[lit_top_peek_bottom(h, gt)]))) continue;
+    }
+    const int bl = cx.lab[buf][i];
+    const int bflg = cx.flg[buf][i];
+    for (int l = 0; l < C; ++l) {
+      if (l == blank) continue;
+      int c = -1;
+      for (int k = cx.head[i]; k >= 0; k = cx.sib[k])
+        if (cx.lab[buf][k] == l) { c = k; break; }
+      int slot;
+      const bool fresh_slot = (c < 0);
+      if (!fresh_slot) {
+        slot = c;
+        if (cx.et[c] != NI) continue;            // c.Active()
+      } else {
+        slot = cx.freel[nfree - 1];
+        cx.eflg[slot] = 0;
+      }
+      const T xl = cx.row[l];
+      const T p = xl - norm;
+      cx.eb[slot] = NI;
+      const T prev = (l == bl) ? cx.ob[buf][i] : cx.ot[buf][i];
+      cx.el[slot] = xl - norm + prev;
+      const bool recv_fresh = fresh_slot ? true : (cx.ot[buf][c] == NI);
+      const T rs_blank = ((bflg & F_ROOT) && recv_fresh) ? T(0) : NI;
+      Best<T> cd{cx.ecn[slot], cx.ebpn[slot], (cx.eflg[slot] & F_HN) != 0};
+      cand_from(cx, buf, i, 0, p, rs_blank, cd);
+      if (l != bl) cand_from(cx, buf, i, 1, p, NI, cd);
+      cx.ecn[slot] = cd.p; cx.ebpn[slot] = cd.bp;
+      cx.eflg[slot] |= F_HN;
+      cx.et[slot] = cx.el[slot];
+      cx.ekind[slot] = fresh_slot ? (((uint32_t)i << 1) | 1u) : ((uint32_t)c << 1);
+      cx.elab[slot] = l;
+      const T ct = cx.et[slot];
+      if (ct > NI && (h.size() < W || ct > cx.et[lit_top_peek_bottom(h, gt)])) {
+        if (fresh_slot) nfree--;
+        if (h.size() == W) {
+          const int bot = lit_top_peek_bottom(h, gt);
+          cx.et[bot] = NI; cx.eb[bot] = NI; cx.el[bot] = NI;
+          cx.eflg[bot] = 0;
+          if (bot >= nb) cx.freel[nfree++] = bot;
+        }
+        lit_top_push(h, slot, gt);
+      } else {
+        cx.et[slot] = NI; cx.eb[slot] = NI; cx.el[slot] = NI;
+        cx.eflg[slot] = 0;
+        if (!fresh_slot) {
+          cx.ot[buf][c] = NI; cx.ob[buf][c] = NI; cx.ol[buf][c] = NI;
+          cx.flg[buf][c] &= ~(F_HB | F_HN);
+        }
+      }
+    }
+  }
+
+  *n_leaves = h.size();
+  if (last) {
+    const int lim = P < W ? P : W;
+    LitTop tp{cx.tops, 0, lim, kTopUnordered};
+    for (int q = 0; q < h.size(); ++q) lit_top_push(tp, h.e[q], gt);
+    lit_top_extract(tp, gt);
+  }
+  const int n = lit_top_extract(h, gt);
+  // slot -> sorted position (freel reused as the map; -1 = not a leaf)
+  for (int s = 0; s < cx.enc; ++s) cx.freel[s] = -1;
+  for (int k = 0; k < n; ++k) {
+    const int s = cx.heap[k];
+    if (cx.freel[s] >= 0) *err = 1;     // the same entry twice in the beam
+    cx.freel[s] = k;
+    cx.sorted[k] = s;
+  }
+  if (last) {
+    const int lim = (P < *n_leaves) ? P : *n_leaves;
+    for (int q = 0; q < lim; ++q) cx.tops[q] = cx.freel[cx.tops[q]];
+  }
+  return n;
+}
+
+// ---------------------------------------------------------------------------
+template <typename T, int R>
+__global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  Ctx<T> cx;
+  carve(cx, lds, prm.W, (int)prm.C);
+  cx.blank = prm.blank;
+  const int lane = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  const int W = prm.W;
+  const int C = (int)prm.C;
+  const int64_t B = prm.B;
+  const int sl = prm.seq_len[b] > 0 ? prm.seq_len[b] : 0;
+  int* const misc = cx.misc;
+
+  // Reset(): root with newp.total = newp.blank = 0 (decoder.h:213-227)
+  int buf = 0;
+  if (lane == 0) {
+    cx.lab[0][0] = -1; cx.par[0][0] = -1; cx.flg[0][0] = F_ROOT;
+    cx.ot[0][0] = T(0); cx.ob[0][0] = T(0); cx.ol[0][0] = ninf<T>();
+    cx.cb[0][0] = T(0); cx.cn[0][0] = T(0);
+    cx.ha[0][0] = kRootHa; cx.hb[0][0] = kRootHb; cx.pha[0][0] = 0; cx.phb[0][0] = 0;
+    cx.head[0] = -1;
+  }
+  int nb = 1;
+  int literal_steps = 0;
+  int err = 0;
+  int n_leaves = 1;
+  __syncthreads();
+
+  for (int t = 0; t < sl; ++t) {
+    const T* xr = prm.x + ((int64_t)t * B + b) * C;
+    for (int j = lane; j < C; j += 64) cx.row[j] = xr[j];
+    const T norm = prm.norm[(int64_t)t * B + b];
+    __syncthreads();
+    const bool last = (t == sl - 1);
+
+    int n = 0;
+    bool ok = false;
+    if (!prm.force_literal) ok = fast_step<T, R>(cx, buf, nb, norm, &n);
+    __syncthreads();
+    if (!ok) {
+      if (lane == 0) {
+        int e2 = 0, nl = 0;
+        misc[0] = literal_step(cx, buf, nb, norm, last, prm.P, &e2, &nl);
+        misc[1] = e2;
+        misc[2] = nl;
+      }
+      __syncthreads();
+      n = misc[0];
+      err |= misc[1];
+      n_leaves = misc[2];
+      ++literal_steps;
+    } else {
+      n_leaves = n;
+      if (last) {
+        for (int q = lane; q < prm.P && q < n; q += 64) cx.tops[q] = q;
+      }
+    }
+    __syncthreads();
+
+    // ---- commit: records + next frame's branch arrays (sorted order) ----
+    const int nx = buf ^ 1;
+    for (int i = lane; i < nb; i += 64) cx.newpos[i] = -1;
+    __syncthreads();
+    for (int k = lane; k < n; k += 64) {
+      const uint32_t kd = cx.ekind[cx.sorted[k]];
+      if (!(kd & 1u)) cx.newpos[kd >> 1] = k;
+    }
+    for (int q = lane; q < cx.hts; q += 64) cx.htab[q] = -1;
+    __syncthreads();
+    // prefix hashes of the new leaves; new children go into the hash table
+    for (int k = lane; k < n; k += 64) {
+      const uint32_t kd = cx.ekind[cx.sorted[k]];
+      const int src = (int)(kd >> 1);
+      uint64_t ha, hb, pa, pb;
+      if (kd & 1u) {
+        pa = cx.ha[buf][src]; pb = cx.hb[buf][src];
+        hmix(pa, pb, cx.elab[cx.sorted[k]], ha, hb);
+        int q = (int)(ha & (uint64_t)(cx.hts - 1));
+        while (atomicCAS(&cx.htab[q], -1, k) != -1) q = (q + 1) & (cx.hts - 1);
+      } else {
+        ha = cx.ha[buf][src]; hb = cx.hb[buf][src];
+        pa = cx.pha[buf][src]; pb = cx.phb[buf][src];
+      }
+      cx.ha[nx][k] = ha; cx.hb[nx][k] = hb; cx.pha[nx][k] = pa; cx.phb[nx][k] = pb;
+    }
+    __syncthreads();
+    Rec* rout = prm.rec + ((int64_t)b * prm.Tmax + t) * W;
+    for (int k = lane; k < n; k += 64) {
+      const int e = cx.sorted[k];
+      const uint32_t kd = cx.ekind[e];
+      const int src = (int)(kd >> 1);
+      const bool isnew = (kd & 1u) != 0;
+      const int pf = cx.flg[buf][src];
+      int parent, fl;
+      if (isnew) {
+        parent = cx.newpos[src];
+        fl = (pf & F_ROOT) ? F_PROOT : 0;
+      } else {
+        const int pp = cx.par[buf][src];
+        parent = pp >= 0 ? cx.newpos[pp] : -1;
+        fl = pf & (F_ROOT | F_PROOT);
+        if (pp < 0 && !(pf & F_ROOT)) {
+          // the parent node was not in the beam; it may have re-entered this
+          // frame as a new child (the reference finds it through the trie)
+          const uint64_t pa = cx.pha[nx][k], pb = cx.phb[nx][k];
+          for (int q = (int)(pa & (uint64_t)(cx.hts - 1));; q = (q + 1) & (cx.hts - 1)) {
+            const int c = cx.htab[q];
+            if (c < 0) break;
+            if (cx.ha[nx][c] == pa && cx.hb[nx][c] == pb) { parent = c; break; }
+          }
+        }
+      }
+      const int ef = cx.eflg[e];
+      fl |= ef & (F_HB | F_HN);
+      cx.lab[nx][k] = cx.elab[e];
+      cx.par[nx][k] = parent;
+      cx.flg[nx][k] = fl;
+      cx.ot[nx][k] = cx.et[e]; cx.ob[nx][k] = cx.eb[e]; cx.ol[nx][k] = cx.el[e];
+      cx.cb[nx][k] = cx.ecb[e]; cx.cn[nx][k] = cx.ecn[e];
+      Rec rc;
+      rc.link = kd;
+      rc.label = cx.elab[e];
+      rc.bp_blank = (ef & F_HB) ? cx.ebpb[e] : kBpNone;
+      rc.bp_nblank = (ef & F_HN) ? cx.ebpn[e] : kBpNone;
+      rout[k] = rc;
+    }
+    __syncthreads();
+    buf = nx;
+    nb = n;
+    for (int k = lane; k < nb; k += 64) cx.head[k] = -1;
+    __syncthreads();
+    for (int k = lane; k < nb; k += 64) {
+      const int pp = cx.par[buf][k];
+      if (pp >= 0) cx.sib[k] = atomicExch(&cx.head[pp], k);
+    }
+    __syncthreads();
+  }
+
+  // TopPaths outputs (decoder.h:230-261); with no frames the root is the leaf
+  if (sl == 0 && lane == 0) cx.tops[0] = 0;
+  __syncthreads();
+  const int np = (prm.P < n_leaves) ? prm.P : n_leaves;
+  for (int q = lane; q < prm.P; q += 64) {
+    int pos = -1, kind = -1;
+    T lp = T(0);
+    if (q < np) {
+      pos = cx.tops[q];
+      const int f = cx.flg[buf][pos];
+      const bool hb = f & F_HB, hn = f & F_HN;
+      if (hb && hn) kind = (cx.cb[buf][pos] > cx.cn[buf][pos]) ? 0 : 1;
+      else if (hb) kind = 0;
+      else if (hn) kind = 1;
+      lp = cx.ot[buf][pos];
+    }
+    prm.top_pos[b * prm.P + q] = pos;
+    prm.top_kind[b * prm.P + q] = kind;
+    prm.log_prob[b * prm.P + q] = lp;
+  }
+  if (lane == 0) {
+    ItemOut io;
+    io.n_leaves = n_leaves;
+    io.literal_steps = literal_steps;
+    io.error = err;
+    io.pad = 0;
+    prm.item[b] = io;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Softmax normaliser per row (decoder.h:72-80): max, sequential sum of
+// exp(x - max) in T precision, log.  Rows past an item's length are skipped.
+__global__ __launch_bounds__(256) void ctcx_row_norm_f32(const float* __restrict__ x, const int32_t* seq_len,
+                                                        float* __restrict__ norm, int64_t Tmax, int64_t B,
+                                                        int64_t C) {
+  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= Tmax * B) return;
+  const int64_t t = row / B, b = row - t * B;
+  if (t >= seq_len[b]) return;
+  const float* r = x + row * C;
+  float m = r[0];
+  for (int64_t j = 1; j < C; ++j) m = (r[j] > m) ? r[j] : m;
+  float s = 0.0f;
+  for (int64_t j = 0; j < C; ++j) s += gm::expf(r[j] - m);
+  norm[row] = m + gm::logf(s);
+}
+
+// ---------------------------------------------------------------------------
+// Backward walks over the records.  which = 0: decoded labels (LabelSeq,
+// ctc_beam_entry.h:123-136); which = 1: best alignment (AlignmentLabelSeq +
+// the candidate chain, ctc_beam_entry.h:137-152, 190-228).  Output reversed.
+__global__ __launch_bounds__(256) void ctcx_traceback(TraceParams tp) {
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nthreads = tp.B * tp.P * 2;
+  if (tid >= nthreads) return;
+  const int which = (int)(tid & 1);
+  const int64_t bp = tid >> 1;
+  const int64_t b = bp / tp.P;
+  const int p = (int)(bp - b * tp.P);
+  const int sl = tp.seq_len[b] > 0 ? tp.seq_len[b] : 0;
+  int32_t* out = tp.seq + (bp * 2 + which) * tp.Tmax;
+  int len = 0;
+  int k = tp.top_pos[bp];
+  if (sl > 0 && k >= 0 && p < tp.item[b].n_leaves) {
+    const Rec* rb = tp.rec + b * tp.Tmax * tp.W;
+    if (which == 0) {
+      int prev = -1;
+      for (int t = sl - 1; t >= 0; --t) {
+        const Rec r = rb[(int64_t)t * tp.W + k];
+        if (r.link & 1u) {
+          if (!tp.merge || r.label != prev) out[len++] = r.label;
+          prev = r.label;
+        }
+        k = (int)(r.link >> 1);
+      }
+    } else {
+      int kind = tp.top_kind[bp];
+      for (int t = sl - 1; t >= 0 && kind >= 0; --t) {
+        const Rec r = rb[(int64_t)t * tp.W + k];
+        out[len++] = kind == 0 ? tp.blank_label : r.label;
+        const uint32_t q = kind == 0 ? r.bp_blank : r.bp_nblank;
+        if (q >= kBpRestart) break;
+        k = (int)(q >> 1);
+        kind = (int)(q & 1u);
+      }
+    }
+  }
+  tp.len[((int64_t)p * 2 + which) * tp.B + b] = len;
+}
+
+// Exclusive scan of lengths per (path, kind); also totals and maxima.
+// One 256-thread block per (path, kind).  res[(p*2+w)*2 + 0] = total, +1 = max.
+__global__ __launch_bounds__(256) void ctcx_scan(const int32_t* len, int64_t* off, int64_t* res, int64_t B) {
+  __shared__ int64_t s_sum[256];
+  __shared__ int64_t s_max[256];
+  const int64_t pw = blockIdx.x;
+  const int32_t* l = len + pw * B;
+  int64_t* o = off + pw * B;
+  int64_t carry = 0, mx = 0;
+  for (int64_t base = 0; base < B; base += 256) {
+    const int64_t i = base + threadIdx.x;
+    const int64_t v = (i < B) ? l[i] : 0;
+    s_sum[threadIdx.x] = v;
+    s_max[threadIdx.x] = v;
+    __syncthreads();
+    for (int d = 1; d < 256; d <<= 1) {
+      const int64_t a = (threadIdx.x >= (unsigned)d) ? s_sum[threadIdx.x - d] : 0;
+      const int64_t m2 = (threadIdx.x >= (unsigned)d) ? s_max[threadIdx.x - d] : 0;
+      __syncthreads();
+      s_sum[threadIdx.x] += a;
+      s_max[threadIdx.x] = s_max[threadIdx.x] > m2 ? s_max[threadIdx.x] : m2;
+      __syncthreads();
+    }
+    if (i < B) o[i] = carry + s_sum[threadIdx.x] - v;
+    carry += s_sum[255];
+    mx = mx > s_max[255] ? mx : s_max[255];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) { res[pw * 2] = carry; res[pw * 2 + 1] = mx; }
+}
+
+// SparseTensor components (kernels.cc:225-254): one block per (item, path, kind).
+__global__ __launch_bounds__(64) void ctcx_pack(PackParams pp) {
+  const int64_t g = blockIdx.x;                 // ((b * P) + p) * 2 + w
+  const int w = (int)(g & 1);
+  const int64_t bpp = g >> 1;
+  const int64_t b = bpp / pp.P;
+  const int p = (int)(bpp - b * pp.P);
+  const int64_t lidx = ((int64_t)p * 2 + w) * pp.B + b;
+  const int n = pp.len[lidx];
+  const int64_t o = pp.off[lidx];
+  const int32_t* s = pp.seq + (bpp * 2 + w) * pp.Tmax;
+  int64_t* idx = pp.idx[p * 2 + w];
+  int64_t* val = pp.val[p * 2 + w];
+  for (int i = threadIdx.x; i < n; i += 64) {
+    idx[(o + i) * 2] = b;
+    idx[(o + i) * 2 + 1] = i;
+    val[o + i] = s[n - 1 - i];
+  }
+}
+
+}  // namespace ctcx
+
+// ---------------------------------------------------------------------------
+// Launchers (called by the C-ABI layer).
+namespace ctcx {
+
+template <typename T, int R>
+static hipError_t launch_decode_r(const DecodeParams<T>& p, size_t lds, hipStream_t s) {
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)ctcx_beam_decode<T, R>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL((ctcx_beam_decode<T, R>), dim3((unsigned)p.B), dim3(64), lds, s, p);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_decode(const DecodeParams<T>& p, hipStream_t s) {
+  const size_t lds = decode_lds_bytes(p.W, p.C, (int)sizeof(T));
+  if (p.B == 0) return hipSuccess;
+  if (p.W <= 64) return launch_decode_r<T, 1>(p, lds, s);
+  if (p.W <= 128) return launch_decode_r<T, 2>(p, lds, s);
+  if (p.W <= 256) return launch_decode_r<T, 4>(p, lds, s);
+  return launch_decode_r<T, 8>(p, lds, s);
+}
+
+template hipError_t launch_decode<float>(const DecodeParams<float>&, hipStream_t);
+template hipError_t launch_decode<double>(const DecodeParams<double>&, hipStream_t);
+
+hipError_t launch_row_norm_f32(const float* x, const int32_t* sl, float* norm, int64_t T, int64_t B, int64_t C,
+                               hipStream_t s) {
+  const int64_t rows = T * B;
+  if (rows == 0) return hipSuccess;
+  hipLaunchKernelGGL(ctcx_row_norm_f32, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, x, sl, norm, T, B, C);
+  return hipGetLastError();
+}
+
+hipError_t launch_traceback(const TraceParams& tp, hipStream_t s) {
+  const int64_t n = tp.B * tp.P * 2;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(ctcx_traceback, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tp);
+  return hipGetLastError();
+}
+
+hipError_t launch_scan(const int32_t* len, int64_t* off, int64_t* res, int64_t B, int P, hipStream_t s) {
+  hipLaunchKernelGGL(ctcx_scan, dim3((unsigned)(P * 2)), dim3(256), 0, s, len, off, res, B);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack(const PackParams& pp, hipStream_t s) {
+  const int64_t n = pp.B * pp.P * 2;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(ctcx_pack, dim3((unsigned)n), dim3(64), 0, s, pp);
+  return hipGetLastError();
+}
+
+}  // namespace ctcx

@@ -1,0 +1,94 @@
+// ctcx_kernels.h — shared declarations between the HIP kernels
+// (ctcx_decode.hip) and the C-ABI host layer (ctcext_capi.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ctcx {
+
+// One record per (item, frame, surviving beam), written in the beam's sorted
+// position k (= its branch index next frame).  16 B so a lane stores it with
+// one dwordx4.  See DESIGN.md "records".
+struct Rec {
+  uint32_t link;    // (src branch << 1) | is_new_child  (prefix back-link)
+  int32_t label;    // the beam's last label (its prefix node's label)
+  uint32_t bp_blank;   // best blank-ending alignment candidate backpointer
+  uint32_t bp_nblank;  // best label-ending alignment candidate backpointer
+};
+constexpr uint32_t kBpRestart = 0xFFFFFFFEu;  // candidate started a new chain
+constexpr uint32_t kBpNone = 0xFFFFFFFFu;     // no candidate of that kind
+
+// Per-item results of the decode kernel.
+struct ItemOut {
+  int32_t n_leaves;       // leaves_.size() after the last frame
+  int32_t literal_steps;  // frames replayed through the literal TopN model
+  int32_t error;          // 0 ok, 1 = unsupported duplicate-beam state
+  int32_t pad;
+};
+
+template <typename T>
+struct DecodeParams {
+  const T* x;               // [Tmax][B][C]
+  const T* norm;            // [Tmax][B]  softmax normaliser per row
+  const int32_t* seq_len;   // [B]
+  int64_t Tmax, B, C;
+  int32_t W, P, blank, blank_label;
+  int32_t force_literal;    // testing knob: replay every frame literally
+  Rec* rec;                 // [B][Tmax][W]
+  ItemOut* item;            // [B]
+  int32_t* top_pos;         // [B][P]  sorted position of path p at the last frame
+  int32_t* top_kind;        // [B][P]  0 blank / 1 label-ending / -1 none
+  T* log_prob;              // [B][P]
+};
+
+struct TraceParams {
+  const Rec* rec;
+  const ItemOut* item;
+  const int32_t* seq_len;
+  const int32_t* top_pos;
+  const int32_t* top_kind;
+  int64_t Tmax, B;
+  int32_t W, P, merge, blank_label;
+  int32_t* seq;    // [B][P][2][Tmax]  walk output, reversed
+  int32_t* len;    // [P][2][B]
+};
+
+struct PackParams {
+  const int32_t* seq;       // as TraceParams::seq
+  const int32_t* len;       // [P][2][B]
+  const int64_t* off;       // [P][2][B] exclusive prefix sums
+  int64_t Tmax, B;
+  int32_t P;
+  int64_t* const* idx;      // [P*2] -> int64 [n][2]   (decoded p, alignment p)
+  int64_t* const* val;      // [P*2] -> int64 [n]
+};
+
+// Size of the per-frame LDS hash table of new leaves (power of two >= 2W).
+__host__ __device__ inline int htab_size(int W) {
+  int n = 16;
+  while (n < 2 * W) n <<= 1;
+  return n;
+}
+
+// LDS bytes needed by the decode kernel (host + device agree on the carve).
+__host__ __device__ inline size_t decode_lds_bytes(int W, int64_t C, int tsize) {
+  const size_t ENC = 2 * (size_t)W + 2;
+  auto a16 = [](size_t v) { return (v + 15) & ~(size_t)15; };
+  size_t s = 0;
+  s += 2 * a16(5 * (size_t)W * tsize);          // branch probs, 2 buffers
+  s += 2 * a16(3 * (size_t)W * 4);              // branch label/parent/flags, 2 buffers
+  s += a16(4 * (size_t)W * 4);                  // head, sib, bstate, newpos
+  s += a16(5 * ENC * tsize);                    // entry probs
+  s += a16(5 * ENC * 4);                        // entry bps/kind/label/flags
+  s += a16(((size_t)W + 1) * 4) * 2;            // heap, top-paths scratch
+  s += a16(ENC * 4);                            // free list / slot map
+  s += a16((size_t)W * 4);                      // sorted
+  s += a16((size_t)C * tsize);                  // logit row
+  s += 64;                                      // scalars
+  s += 2 * 4 * (size_t)W * 8;                   // prefix hashes (own + parent), 2 buffers
+  s += 4 * (size_t)htab_size(W);                // per-frame new-leaf hash table
+  return s;
+}
+
+}  // namespace ctcx

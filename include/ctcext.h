@@ -1,0 +1,118 @@
+/* ctcext.h — C ABI of the MI355X CTC beam-search decoder with per-beam
+ * best-alignment tracking (libctcext.so).
+ *
+ * This is the drop-in boundary for the reference TensorFlow op
+ *   REGISTER_OP("CTCExtBeamSearchDecoder")
+ *       cc/ops/ctc_ext_beam_search_decoder_ops.cc:9-63
+ *   CTCExtBeamSearchDecoderOp<T>::Compute
+ *       cc/kernels/ctc_ext_beam_search_decoder_kernels.cc:20-95
+ * (paths relative to /root/reference/tensorflow_ctc_ext_beam_search_decoder/).
+ * Plain pointers and sizes only; no framework types cross it.  A TF OpKernel
+ *  or the ctypes binding in ctcext_amd/_lib.py calls it.
+ *
+ * Two phases, like the reference kernel which counts entries before
+ * allocating its outputs (kernels.cc:170-213):
+ *   1. ctcext_decode: validates, decodes the whole batch on the GPU and
+ *      returns, per top path, the SparseTensor entry counts and dense widths.
+ *   2. ctcext_fetch: writes the int64 SparseTensor components and the
+ *      log-probabilities into caller-allocated buffers (device or host).
+ * Status codes are TensorFlow's (error::Code); messages are the reference's
+ * verbatim (kernels.cc:111-139, ctc_ext_beam_search_decoder.h:237-243).
+ */
+#ifndef CTCEXT_H_
+#define CTCEXT_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  CTCEXT_OK = 0,
+  CTCEXT_INVALID_ARGUMENT = 3,   /* errors::InvalidArgument */
+  CTCEXT_FAILED_PRECONDITION = 9,/* errors::FailedPrecondition */
+  CTCEXT_UNIMPLEMENTED = 12,
+  CTCEXT_INTERNAL = 13
+};
+
+enum { CTCEXT_F32 = 0, CTCEXT_F64 = 1 };   /* attr T: {float, double} (ops.cc:24) */
+
+enum {
+  CTCEXT_FLAG_FORCE_LITERAL = 1,   /* testing: replay every frame through the literal TopN model */
+  CTCEXT_FLAG_PROFILE = 2          /* time the decode kernel with HIP events (ctcext_stats) */
+};
+
+typedef struct ctcext_decoder ctcext_decoder;
+
+/* Replaces the op's inputs + attrs (ops.cc:10-17). */
+typedef struct {
+  int32_t dtype;                   /* CTCEXT_F32 / CTCEXT_F64 */
+  int32_t inputs_on_device;        /* 1: inputs/sequence_length are device (HBM) pointers */
+  const void* inputs;              /* [max_time, batch_size, num_classes] row-major */
+  const int32_t* sequence_length;  /* [batch_size] */
+  int64_t max_time, batch_size, num_classes;
+  int32_t beam_width;              /* attr beam_width >= 1 */
+  int32_t top_paths;               /* attr top_paths >= 1 */
+  int32_t merge_repeated;          /* attr merge_repeated (default false) */
+  int32_t blank_index;             /* attr blank_index (default 0) */
+  int32_t blank_label;             /* attr blank_label (default -1) */
+  int32_t flags;                   /* CTCEXT_FLAG_* */
+  void* stream;                    /* hipStream_t; NULL = the decoder's own stream */
+} ctcext_decode_args;
+
+/* Per top path p: sizes of decoded_indices[p] ([num_decoded, 2]),
+ * decoded_values[p] ([num_decoded]), decoded_shape[p] = {batch, max_decoded},
+ * and the same for the alignment outputs. */
+typedef struct {
+  int64_t num_decoded, max_decoded;
+  int64_t num_alignment, max_alignment;
+} ctcext_path_sizes;
+
+/* Replaces the op's 6 * top_paths + 1 outputs (ops.cc:18-24).  Each list is an
+ * array of top_paths pointers; shapes as in ctcext_path_sizes. */
+typedef struct {
+  int32_t outputs_on_device;       /* 1: all pointers below are device pointers */
+  int64_t* const* decoded_indices;
+  int64_t* const* decoded_values;
+  int64_t* const* decoded_shape;
+  int64_t* const* alignment_indices;
+  int64_t* const* alignment_values;
+  int64_t* const* alignment_shape;
+  void* log_probability;           /* [batch_size, top_paths] of dtype */
+} ctcext_outputs;
+
+typedef struct {
+  int64_t literal_frames;          /* frames replayed through the literal TopN model */
+  int64_t no_label_paths;          /* paths whose alignment is empty: the reference prints
+                                      "No label seq available" (ctc_beam_entry.h:148-150) */
+  double decode_kernel_ms;         /* with CTCEXT_FLAG_PROFILE: last ctcx_beam_decode time */
+  double norm_kernel_ms;
+  double traceback_ms;             /* traceback + scan */
+} ctcext_stats;
+
+/* Handle lifetime.  A handle owns a HIP stream and a grow-only device
+ * workspace; it is not thread-safe (use one per thread, like an OpKernel). */
+int ctcext_create(int device, ctcext_decoder** out);
+void ctcext_destroy(ctcext_decoder* dec);
+
+/* Phase 1 (Compute up to the allocation of the outputs).  Synchronous. */
+int ctcext_decode(ctcext_decoder* dec, const ctcext_decode_args* args, ctcext_path_sizes* sizes);
+
+/* Phase 2 (StoreAllDecodedSequences + log_probability).  Synchronous. */
+int ctcext_fetch(ctcext_decoder* dec, const ctcext_outputs* out);
+
+int ctcext_get_stats(ctcext_decoder* dec, ctcext_stats* stats);
+
+/* Message of the last failing call on this thread ("" if none). */
+const char* ctcext_last_error(void);
+
+/* Maximum beam width supported on this device for the given class count and
+ * dtype (the per-item beam state is LDS-resident). */
+int32_t ctcext_max_beam_width(int64_t num_classes, int32_t dtype);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CTCEXT_H_ */

@@ -41,6 +41,7 @@
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -244,6 +245,22 @@ class Decoder {
 
     std::vector<N*> branches = leaves_.extract();
     leaves_.reset();
+    if (getenv("ORACLE_DUPCHECK")) {   // debugging aid: duplicate entries in the beam
+      std::vector<N*> sb(branches);
+      std::sort(sb.begin(), sb.end());
+      if (std::adjacent_find(sb.begin(), sb.end()) != sb.end()) printf("DUPLICATE ENTRY IN BEAM\n");
+    }
+    if (getenv("ORACLE_TRACE")) {   // debugging aid: frame-start beam, extract order
+      printf("frame\n");
+      for (N* b : branches) {
+        std::vector<int> pre;
+        for (N* c = b; c->parent; c = c->parent) pre.push_back(c->label);
+        std::reverse(pre.begin(), pre.end());
+        printf("  %a [", (double)b->new_t);
+        for (int v : pre) printf("%d,", v);
+        printf("]\n");
+      }
+    }
     for (N* b : branches) {
       b->old_t = b->new_t; b->old_b = b->new_b; b->old_l = b->new_l;
       b->old_c = b->new_c;
