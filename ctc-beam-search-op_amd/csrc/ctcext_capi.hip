@@ -225,6 +225,9 @@ static int run_decode(ctcext_decoder* d, const ctcext_decode_args* a, const T* x
                   "beam reached a state holding the same entry twice (only reachable with -inf "
                   "totals); not supported on the device path");
     d->stats.literal_frames += io[b].literal_steps;
+    d->stats.literal_nonfinite += io[b].why_nonfinite;
+    d->stats.literal_evict_tie += io[b].why_evict_tie;
+    d->stats.literal_order_tie += io[b].why_order_tie;
   }
   // TopPaths (decoder.h:240-243) fails on the first item with too few leaves
   for (int64_t b = 0; b < B; ++b)

@@ -93,6 +93,11 @@ struct Best {
   }
 };
 
+// One TopN element: the entry's total travels with its slot id.
+template <typename T> struct HE;
+template <> struct __attribute__((aligned(8))) HE<float> { float v; int s; };
+template <> struct __attribute__((aligned(16))) HE<double> { double v; int s; int pad; };
+
 template <typename T>
 struct Ctx {
   // branch arrays, double-buffered by frame parity: [buf][i]
@@ -109,6 +114,7 @@ struct Ctx {
   // parent's, [buf][i]; htab maps the hash of a frame's new leaves to position
   uint64_t* ha[2]; uint64_t* hb[2]; uint64_t* pha[2]; uint64_t* phb[2];
   int* htab;
+  HE<T>* he;           // TopN elements_, position p at he[p + 1]
   int W, C, blank, enc, hts;
 };
 
@@ -174,6 +180,8 @@ __host__ __device__ void carve(Ctx<T>& cx, char* base, int W, int C) {
   }
   cx.hts = htab_size(W);
   cx.htab = (int*)p;
+  p += a16(4 * (size_t)cx.hts);
+  cx.he = (HE<T>*)p;
   cx.W = W; cx.C = C; cx.enc = (int)ENC;
 }
 
@@ -244,54 +252,177 @@ __host__ __device__ void recurse_branch(const Ctx<T>& cx, int buf, int i, T norm
 }
 
 // ---------------------------------------------------------------------------
-// FAST path for one frame (whole wave).  Returns false if the frame must be
-// replayed literally.  On success cx.sorted[0..*n_out) holds the surviving
-// entry slots in descending total order.
-template <typename T, int R>
-__device__ bool fast_step(Ctx<T>& cx, int buf, int nb, T norm, int* n_out) {
+// Exact TopN heap operations on LDS (position p of gtl::TopN::elements_ lives
+// at he[p + 1], so the two children of node h, positions 2h+1 and 2h+2, are
+// one 16-byte aligned pair).  Values travel with the slot id, exactly as the
+// reference compares BeamEntry* through their newp.total.
+
+// libstdc++ __adjust_heap + __push_heap, one lane, on positions [0, len).
+template <typename T>
+__device__ void lane_adjust_heap(HE<T>* he, int hole, int len, HE<T> value) {
+  const int top = hole;
+  int second = hole;
+  while (second < (len - 1) / 2) {
+    second = 2 * (second + 1);
+    if (he[second + 1].v > he[second].v) second--;
+    he[hole + 1] = he[second + 1];
+    hole = second;
+  }
+  if ((len & 1) == 0 && second == (len - 2) / 2) {
+    second = 2 * (second + 1);
+    he[hole + 1] = he[second];
+    hole = second - 1;
+  }
+  int parent = (hole - 1) / 2;
+  while (hole > top && he[parent + 1].v > value.v) {
+    he[hole + 1] = he[parent + 1];
+    hole = parent;
+    parent = (hole - 1) / 2;
+  }
+  he[hole + 1] = value;
+}
+
+// std::make_heap over [0, len).  Parents at one depth own disjoint subtrees,
+// so each level's sift-downs run in parallel lanes (deepest level first, the
+// order libstdc++ visits them in).
+template <typename T>
+__device__ void wave_make_heap(HE<T>* he, int len) {
+  if (len < 2) return;
+  const int last = (len - 2) / 2;
+  const int dmax = 31 - __builtin_clz((unsigned)(last + 1));
+  for (int d = dmax; d >= 0; --d) {
+    const int lo = (1 << d) - 1;
+    const int hi = min((1 << (d + 1)) - 2, last);
+    for (int i = lo + (int)threadIdx.x; i <= hi; i += 64) lane_adjust_heap(he, i, len, he[i + 1]);
+  }
+}
+
+// __adjust_heap(top, len, v) for the whole wave.  The hole descends along the
+// smaller child (right on ties) to a leaf and v then rises while its parent is
+// strictly greater; since values along that path are non-decreasing this is
+// "walk the min-child path while the child is <= v".  Every lane computes the
+// min child of its internal nodes in parallel (one LDS pair read each); the
+// walk is a uniform readlane chase.  Requires finite values below `top`.
+template <typename T, int RN>
+__device__ void wave_adjust_heap(HE<T>* he, int top, int len, HE<T> v) {
+  const int lane = threadIdx.x;
+  const int nint = len / 2;   // nodes with at least one child
+  int nx[RN];
+  T cv[RN];
+  int cs[RN];
+#pragma unroll
+  for (int r = 0; r < RN; ++r) {
+    const int i = r * 64 + lane;
+    nx[r] = -1; cv[r] = T(0); cs[r] = 0;
+    if (i < nint && i >= top) {
+      const HE<T> L = he[2 * i + 2];
+      int c = 2 * i + 1;
+      HE<T> ch = L;
+      if (2 * i + 2 < len) {
+        const HE<T> Rt = he[2 * i + 3];
+        if (!(Rt.v > L.v)) { c = 2 * i + 2; ch = Rt; }
+      }
+      nx[r] = c; cv[r] = ch.v; cs[r] = ch.s;
+    }
+  }
+  int p = top;
+  while (p < nint) {
+    const int rr = p >> 6, l = p & 63;
+    int q = nx[0];
+    T a = cv[0];
+    int sl = cs[0];
+#pragma unroll
+    for (int r = 1; r < RN; ++r)
+      if (rr == r) { q = nx[r]; a = cv[r]; sl = cs[r]; }
+    q = bcast(q, l);
+    a = bcast(a, l);
+    sl = bcast(sl, l);
+    if (a > v.v) break;
+    if (lane == 0) he[p + 1] = HE<T>{a, sl};
+    p = q;
+  }
+  if (lane == 0) he[p + 1] = v;
+}
+
+// peek_bottom() in the UNORDERED state: the first minimum moves to the front.
+template <typename T>
+__device__ void wave_first_min_to_front(HE<T>* he, int n) {
+  const int lane = threadIdx.x;
+  T mv = pinf<T>();
+  int mi = 0x7fffffff;
+  for (int i = lane; i < n; i += 64) {
+    const T v = he[i + 1].v;
+    if (v < mv) { mv = v; mi = i; }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const T ov = __shfl_xor(mv, o);
+    const int oi = __shfl_xor(mi, o);
+    if (ov < mv || (ov == mv && oi < mi)) { mv = ov; mi = oi; }
+  }
+  if (mi != 0 && lane == 0) {
+    const HE<T> a = he[1];
+    he[1] = he[mi + 1];
+    he[mi + 1] = a;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// EXACT fast path for one frame (whole wave): the reference's Step with its
+// TopN replayed operation for operation (so ties resolve as in the
+// reference), offers scored and filtered in parallel.  Returns 0 on success,
+// else the reason the frame goes to literal_step: 1 = a non-finite logit or
+// total, 2 = the beam fills up in the middle of the grow loop (the reference
+// then peeks lazily; rare: only while the beam is still filling).
+// On success cx.sorted[0..*n_out) holds the Extract() order and, for the last
+// frame, cx.tops[0..min(P, leaves)) the TopPaths() selection as positions.
+template <typename T, int RN>
+__device__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, bool last, int P, int* n_out,
+                          int* n_leaves) {
   const int lane = threadIdx.x;
   const T NI = ninf<T>();
   const int W = cx.W;
   const int C = cx.C;
   const int blank = cx.blank;
+  HE<T>* he = cx.he;
 
-  // roll + recursion, lanes over branches
-  for (int r = 0; r < R; ++r) {
-    const int i = r * 64 + lane;
-    if (i < nb) {
-      cx.et[i] = cx.ot[buf][i]; cx.eb[i] = cx.ob[buf][i]; cx.el[i] = cx.ol[buf][i];
-      cx.eflg[i] = 0;
-      cx.bst[i] = 0;
-    }
+  bool bad = !(norm > NI && norm < pinf<T>());
+  for (int j = lane; j < C; j += 64) {
+    const T xv = cx.row[j];
+    bad |= (xv != xv) || (xv == pinf<T>());
+  }
+  if (__ballot(bad)) return 1;
+
+  // roll (decoder.h:87-92) + recursion (decoder.h:95-143), lanes over branches
+  for (int i = lane; i < nb; i += 64) {
+    cx.et[i] = cx.ot[buf][i]; cx.eb[i] = cx.ob[buf][i]; cx.el[i] = cx.ol[buf][i];
+    cx.eflg[i] = 0;
+    cx.bst[i] = 0;
   }
   __syncthreads();
-  for (int r = 0; r < R; ++r) {
-    const int i = r * 64 + lane;
-    if (i < nb) recurse_branch(cx, buf, i, norm, false);
+  for (int i = lane; i < nb; i += 64) recurse_branch(cx, buf, i, norm, false);
+  __syncthreads();
+  bool nonfinite = false;
+  for (int i = lane; i < nb; i += 64) {
+    const T v = cx.et[i];
+    nonfinite |= !(v > NI && v < pinf<T>());
+    he[i + 1] = HE<T>{v, i};           // leaves_.push(b) in branch order
   }
+  for (int k = lane; k < cx.enc - nb; k += 64) cx.freel[k] = nb + k;
+  if (__ballot(nonfinite)) return 1;
   __syncthreads();
 
-  T val[R];
-  bool finite = true;
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int e = r * 64 + lane;
-    val[r] = (e < nb) ? cx.et[e] : pinf<T>();
-    if (e < nb && !(val[r] > NI && val[r] < pinf<T>())) finite = false;
+  int n = nb;                     // elements_.size()
+  int nfree = cx.enc - nb;
+  int st = kTopUnordered;
+  bool full = (n >= W);
+  if (full) {                     // branch 0's is_candidate() peeks
+    wave_first_min_to_front(he, n);
+    st = kTopBottomKnown;
   }
-  if (__ballot(!finite)) return false;
+  T bottom = full ? he[1].v : NI;
 
-  int size = nb;
-  bool full = (size >= W);
-  T bottom = NI;
-  if (full) {
-    T m = val[0];
-#pragma unroll
-    for (int r = 1; r < R; ++r) m = (val[r] < m) ? val[r] : m;
-    bottom = wave_min(m);
-  }
-
-  // grow: offers in (branch order, label order), 64 per chunk
+  // grow (decoder.h:146-209): offers in (branch order, label order)
   const int Cm1 = C - 1;
   const int64_t total = (int64_t)nb * Cm1;
   for (int64_t f0 = 0; f0 < total; f0 += 64) {
@@ -335,74 +466,107 @@ __device__ bool fast_step(Ctx<T>& cx, int buf, int nb, T norm, int* n_out) {
       const T k_s = bcast(s, k);
       const bool accept = k_isbc ? (k_s > NI && (!full || k_s > bottom)) : true;
       if (accept) {
-        int pos;
-        if (!full) {
-          pos = size++;
+        int slot;
+        if (k_isbc) {
+          slot = k_c;
         } else {
-          // the unique minimum is evicted; a tie at the minimum is layout-dependent
-          int cnt = 0;
-          pos = -1;
-#pragma unroll
-          for (int r = 0; r < R; ++r) {
-            const uint64_t mm = __ballot(val[r] == bottom);
-            cnt += __popcll(mm);
-            if (pos < 0 && mm) pos = r * 64 + __ffsll((unsigned long long)mm) - 1;
+          slot = cx.freel[nfree - 1];
+          --nfree;
+        }
+        if (full) {
+          // evict the bottom (decoder.h:192-198): it is the front
+          const int fslot = he[1].s;
+          if (lane == 0) {
+            cx.et[fslot] = NI; cx.eb[fslot] = NI; cx.el[fslot] = NI; cx.eflg[fslot] = 0;
+            he[1].v = NI;
           }
-          if (cnt != 1) return false;
-          const uint32_t kd = cx.ekind[pos];
-          if (!(kd & 1u)) {
-            const int j = (int)(kd >> 1);
-            if (lane == 0) cx.bst[j] |= S_EVICT;
-            if (isbc && c == j) cev = true;
+          if (fslot < nb) {
+            if (lane == 0) cx.bst[fslot] |= S_EVICT;
+            if (isbc && c == fslot) cev = true;
+          } else {
+            if (lane == 0) cx.freel[nfree] = fslot;
+            ++nfree;
           }
         }
         if (lane == k) {
-          cx.et[pos] = s; cx.eb[pos] = NI; cx.el[pos] = s;
-          cx.ecn[pos] = cd.p; cx.ebpn[pos] = cd.bp;
-          cx.eflg[pos] = F_HN;
-          cx.ekind[pos] = isbc ? ((uint32_t)c << 1) : (((uint32_t)i << 1) | 1u);
-          cx.elab[pos] = l;
+          cx.et[slot] = s; cx.eb[slot] = NI; cx.el[slot] = s;
+          cx.ecn[slot] = cd.p; cx.ebpn[slot] = cd.bp;
+          cx.eflg[slot] = F_HN;
+          cx.ekind[slot] = isbc ? ((uint32_t)c << 1) : (((uint32_t)i << 1) | 1u);
+          cx.elab[slot] = l;
           if (isbc) cx.bst[c] &= ~S_EVICT;
         }
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-          if (r * 64 + lane == pos) val[r] = k_s;
-        if (!full && size == W) full = true;
-        if (full) {
-          T mv = val[0];
-#pragma unroll
-          for (int r = 1; r < R; ++r) mv = (val[r] < mv) ? val[r] : mv;
-          bottom = wave_min(mv);
+        const HE<T> nv{k_s, slot};
+        if (st == kTopHeap) {
+          wave_adjust_heap<T, RN>(he, 0, W, nv);          // push = pop_heap(W + 1)
+        } else {
+          if (lane == 0) he[n + 1] = nv;
+          ++n;
+          if (st == kTopBottomKnown && !(k_s > he[1].v) && lane == 0) {
+            const HE<T> a = he[1];
+            he[1] = he[n];
+            he[n] = a;
+          }
+          if (n == W + 1) {
+            wave_make_heap(he, W + 1);
+            const HE<T> v2 = he[W + 1];
+            if (lane == 0) he[W + 1] = he[1];
+            wave_adjust_heap<T, RN>(he, 0, W, v2);
+            st = kTopHeap;
+          } else if (n == W) {
+            return 2;   // filled mid-frame: the lazy peek is replayed literally
+          }
         }
+        if (full) bottom = he[1].v;
       } else {
         // re-offered evicted branch rejected -> deactivated (decoder.h:200-205)
         if (lane == 0) cx.bst[k_c] |= S_DEACT;
         if (i == k_c) live = false;
       }
-      __syncthreads();
     }
   }
 
-  // final order: rank sort, descending; any equal totals -> literal replay
-  const int n = size;
-  bool tie = false;
-  for (int r = 0; r < R; ++r) {
-    const int e = r * 64 + lane;
-    if (e < n) {
-      const T v = val[r];
-      int rank = 0;
-      for (int q = 0; q < n; ++q) {
-        const T w = cx.et[q];
-        rank += (w > v) ? 1 : 0;
-        tie |= (q != e) && (w == v);
-      }
-      cx.sorted[rank] = e;
+  const int size = n < W ? n : W;
+  *n_leaves = size;
+  // TopPaths (decoder.h:245-252) reads the unsorted layout: lane 0, literal
+  if (last) {
+    if (lane == 0) {
+      for (int q = 0; q < size; ++q) cx.heap[q] = he[q + 1].s;
+      SlotGreater<T> gt{cx.et};
+      const int lim = P < W ? P : W;
+      LitTop tp{cx.tops, 0, lim, kTopUnordered};
+      for (int q = 0; q < size; ++q) lit_top_push(tp, cx.heap[q], gt);
+      lit_top_extract(tp, gt);
+    }
+    __syncthreads();
+  }
+  // Extract() of the next frame (decoder.h:84): sort_heap, or std::sort
+  int nout;
+  if (st == kTopHeap) {
+    for (int len = W; len > 1; --len) {
+      const HE<T> v = he[len];
+      if (lane == 0) he[len] = he[1];
+      wave_adjust_heap<T, RN>(he, 0, len - 1, v);
+    }
+    nout = W;
+    for (int k = lane; k < nout; k += 64) cx.sorted[k] = he[k + 1].s;
+  } else {
+    nout = n;
+    if (lane == 0) {
+      for (int q = 0; q < n; ++q) cx.sorted[q] = he[q + 1].s;
+      lit_sort(cx.sorted, n, SlotGreater<T>{cx.et});
     }
   }
-  if (__ballot(tie)) return false;
   __syncthreads();
-  *n_out = n;
-  return true;
+  if (last && lane == 0) {
+    // TopPaths slots -> sorted positions
+    for (int q = 0; q < nout; ++q) cx.freel[cx.sorted[q]] = q;
+    const int lim = (P < size) ? P : size;
+    for (int q = 0; q < lim; ++q) cx.tops[q] = cx.freel[cx.tops[q]];
+  }
+  __syncthreads();
+  *n_out = nout;
+  return 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -511,7 +675,7 @@ __host__ __device__ int literal_step(Ctx<T>& cx, int buf, int nb, T norm, bool l
 }
 
 // ---------------------------------------------------------------------------
-template <typename T, int R>
+template <typename T, int RN>
 __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   Ctx<T> cx;
@@ -536,6 +700,7 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
   }
   int nb = 1;
   int literal_steps = 0;
+  int why_nf = 0, why_et = 0, why_ot = 0;
   int err = 0;
   int n_leaves = 1;
   __syncthreads();
@@ -548,9 +713,12 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     const bool last = (t == sl - 1);
 
     int n = 0;
-    bool ok = false;
-    if (!prm.force_literal) ok = fast_step<T, R>(cx, buf, nb, norm, &n);
+    int why = 4;
+    int nl_fast = 0;
+    if (!prm.force_literal) why = exact_step<T, RN>(cx, buf, nb, norm, last, prm.P, &n, &nl_fast);
     __syncthreads();
+    const bool ok = (why == 0);
+    why_nf += (why == 1); why_et += (why == 2);
     if (!ok) {
       if (lane == 0) {
         int e2 = 0, nl = 0;
@@ -564,10 +732,7 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
       n_leaves = misc[2];
       ++literal_steps;
     } else {
-      n_leaves = n;
-      if (last) {
-        for (int q = lane; q < prm.P && q < n; q += 64) cx.tops[q] = q;
-      }
+      n_leaves = nl_fast;
     }
     __syncthreads();
 
@@ -675,7 +840,10 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     io.n_leaves = n_leaves;
     io.literal_steps = literal_steps;
     io.error = err;
-    io.pad = 0;
+    io.why_nonfinite = why_nf;
+    io.why_evict_tie = why_et;
+    io.why_order_tie = why_ot;
+    io.pad[0] = io.pad[1] = 0;
     prm.item[b] = io;
   }
 }
@@ -798,14 +966,14 @@ __global__ __launch_bounds__(64) void ctcx_pack(PackParams pp) {
 // Launchers (called by the C-ABI layer).
 namespace ctcx {
 
-template <typename T, int R>
+template <typename T, int RN>
 static hipError_t launch_decode_r(const DecodeParams<T>& p, size_t lds, hipStream_t s) {
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)ctcx_beam_decode<T, R>,
+    hipError_t e = hipFuncSetAttribute((const void*)ctcx_beam_decode<T, RN>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((ctcx_beam_decode<T, R>), dim3((unsigned)p.B), dim3(64), lds, s, p);
+  hipLaunchKernelGGL((ctcx_beam_decode<T, RN>), dim3((unsigned)p.B), dim3(64), lds, s, p);
   return hipGetLastError();
 }
 
@@ -813,10 +981,10 @@ template <typename T>
 hipError_t launch_decode(const DecodeParams<T>& p, hipStream_t s) {
   const size_t lds = decode_lds_bytes(p.W, p.C, (int)sizeof(T));
   if (p.B == 0) return hipSuccess;
-  if (p.W <= 64) return launch_decode_r<T, 1>(p, lds, s);
-  if (p.W <= 128) return launch_decode_r<T, 2>(p, lds, s);
-  if (p.W <= 256) return launch_decode_r<T, 4>(p, lds, s);
-  return launch_decode_r<T, 8>(p, lds, s);
+  // RN registers per lane hold the min-child of the (W + 1) / 2 internal heap nodes
+  if (p.W <= 128) return launch_decode_r<T, 1>(p, lds, s);
+  if (p.W <= 256) return launch_decode_r<T, 2>(p, lds, s);
+  return launch_decode_r<T, 4>(p, lds, s);
 }
 
 template hipError_t launch_decode<float>(const DecodeParams<float>&, hipStream_t);

@@ -24,7 +24,10 @@ struct ItemOut {
   int32_t n_leaves;       // leaves_.size() after the last frame
   int32_t literal_steps;  // frames replayed through the literal TopN model
   int32_t error;          // 0 ok, 1 = unsupported duplicate-beam state
-  int32_t pad;
+  int32_t why_nonfinite;  // literal replays caused by a non-finite total
+  int32_t why_evict_tie;  // ... by equal totals at an eviction
+  int32_t why_order_tie;  // ... by equal totals in the final order
+  int32_t pad[2];
 };
 
 template <typename T>
@@ -87,7 +90,8 @@ __host__ __device__ inline size_t decode_lds_bytes(int W, int64_t C, int tsize) 
   s += a16((size_t)C * tsize);                  // logit row
   s += 64;                                      // scalars
   s += 2 * 4 * (size_t)W * 8;                   // prefix hashes (own + parent), 2 buffers
-  s += 4 * (size_t)htab_size(W);                // per-frame new-leaf hash table
+  s += a16(4 * (size_t)htab_size(W));           // per-frame new-leaf hash table
+  s += ((size_t)W + 2) * (tsize == 8 ? 16 : 8); // TopN elements (value, slot)
   return s;
 }
 

@@ -55,7 +55,9 @@ class Outputs(ctypes.Structure):
 
 
 class Stats(ctypes.Structure):
-    _fields_ = [("literal_frames", ctypes.c_int64), ("no_label_paths", ctypes.c_int64),
+    _fields_ = [("literal_frames", ctypes.c_int64), ("literal_nonfinite", ctypes.c_int64),
+                ("literal_evict_tie", ctypes.c_int64), ("literal_order_tie", ctypes.c_int64),
+                ("no_label_paths", ctypes.c_int64),
                 ("decode_kernel_ms", ctypes.c_double), ("norm_kernel_ms", ctypes.c_double),
                 ("traceback_ms", ctypes.c_double)]
 

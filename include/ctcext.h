@@ -84,6 +84,9 @@ typedef struct {
 
 typedef struct {
   int64_t literal_frames;          /* frames replayed through the literal TopN model */
+  int64_t literal_nonfinite;       /*   ... because a beam total was not finite */
+  int64_t literal_evict_tie;       /*   ... because the evicted bottom was tied */
+  int64_t literal_order_tie;       /*   ... because two surviving totals were equal */
   int64_t no_label_paths;          /* paths whose alignment is empty: the reference prints
                                       "No label seq available" (ctc_beam_entry.h:148-150) */
   double decode_kernel_ms;         /* with CTCEXT_FLAG_PROFILE: last ctcx_beam_decode time */

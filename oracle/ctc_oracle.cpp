@@ -128,9 +128,11 @@ class BoundedTop {
 // ---------------------------------------------------------------------------
 // Alignment candidate stores.
 template <class T>
-struct VecCand {             // reference-shaped candidate
+struct VecCand {             // reference-shaped candidate (ctc_beam_entry.h:46-63)
   T prob;
   std::vector<int> seq;
+  VecCand() : prob(LogZero<T>()) {}
+  VecCand(std::vector<int> s, T p) : prob(p), seq(s) {}   // by value, then copied: as the reference
 };
 template <class T>
 struct VecCandLess {
@@ -145,19 +147,24 @@ struct FaithfulStore {
   static T prob(const Slots& s, int k) { return s.q[k].top().prob; }
   static void clear(Slots& s) { s.q[0] = Queue(); s.q[1] = Queue(); }
   // dst gets candidate (base(src,k) + p, base.seq ++ [label])
+  static VecCand<T> top_copy(const Queue& q) { VecCand<T> r = q.top(); return r; }
+  // Same allocation/copy pattern as the reference's AddAlignmentCandidate
+  // (ctc_beam_entry.h:190-228), so its O(t) copies per call are reproduced.
   void add(Slots& dst, int to_k, const Slots& src, int from_k, T base_if_none, T p, int label) {
-    std::vector<int> seq;
+    VecCand<T> old_cand;
+    std::vector<int> old_seq;
     T base;
     if (!src.q[from_k].empty()) {
-      VecCand<T> c = src.q[from_k].top();   // copies, like GetBlank/GetNBlank
-      base = c.prob;
-      seq = c.seq;
+      old_cand = top_copy(src.q[from_k]);
+      base = old_cand.prob;
+      old_seq = old_cand.seq;
     } else {
       base = base_if_none;
     }
-    std::vector<int> grown(seq);
+    std::vector<int> grown(old_seq);
     grown.push_back(label);
-    dst.q[to_k].push(VecCand<T>{base + p, grown});
+    VecCand<T> nc = VecCand<T>(grown, base + p);
+    dst.q[to_k].push(nc);
   }
   std::vector<int> sequence(const Slots& s, int k) const { return s.q[k].top().seq; }
   void reset_all() {}
