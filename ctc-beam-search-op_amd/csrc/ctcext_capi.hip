@@ -90,7 +90,7 @@ struct ctcext_decoder {
   int device = 0;
   hipStream_t own_stream = nullptr;
   // workspace
-  DevBuf x, sl, norm, rec, item, top_pos, top_kind, logp, seq, len, off, res, ptrs, out_idx, out_val;
+  DevBuf x, sl, norm, rec, item, top_pos, top_kind, logp, seq, len, off, res, ptrs, out_idx, out_val, phase;
   HostBuf h_item, h_res;
   hipEvent_t ev[6] = {};
   // state of the last successful decode (consumed by fetch)
@@ -137,7 +137,7 @@ extern "C" void ctcext_destroy(ctcext_decoder* d) {
   (void)hipSetDevice(d->device);
   if (d->own_stream) (void)hipStreamSynchronize(d->own_stream);
   DevBuf* bufs[] = {&d->x, &d->sl, &d->norm, &d->rec, &d->item, &d->top_pos, &d->top_kind, &d->logp,
-                    &d->seq, &d->len, &d->off, &d->res, &d->ptrs, &d->out_idx, &d->out_val};
+                    &d->seq, &d->len, &d->off, &d->res, &d->ptrs, &d->out_idx, &d->out_val, &d->phase};
   for (DevBuf* b : bufs) b->release();
   d->h_item.release();
   d->h_res.release();
@@ -148,6 +148,15 @@ extern "C" void ctcext_destroy(ctcext_decoder* d) {
 }
 
 extern "C" const char* ctcext_last_error(void) { return g_err.c_str(); }
+
+extern "C" int ctcext_phase_counters(ctcext_decoder* d, uint64_t* out, int64_t n) {
+  if (!d || !out) return fail(CTCEXT_INVALID_ARGUMENT, "null argument");
+  if (!d->phase.p) return fail(CTCEXT_FAILED_PRECONDITION, "no CTCEXT_FLAG_PHASES decode yet");
+  if (n < 0 || 8 * (size_t)n > d->phase.cap) return fail(CTCEXT_INVALID_ARGUMENT, "n exceeds the counter buffer");
+  HIP_OR_FAIL(hipSetDevice(d->device));
+  HIP_OR_FAIL(hipMemcpy(out, d->phase.p, 8 * (size_t)n, hipMemcpyDeviceToHost));
+  return CTCEXT_OK;
+}
 
 extern "C" int ctcext_get_stats(ctcext_decoder* d, ctcext_stats* s) {
   if (!d || !s) return fail(CTCEXT_INVALID_ARGUMENT, "null argument");
@@ -194,6 +203,11 @@ static int run_decode(ctcext_decoder* d, const ctcext_decode_args* a, const T* x
   p.top_pos = (int32_t*)d->top_pos.p;
   p.top_kind = (int32_t*)d->top_kind.p;
   p.log_prob = (T*)d->logp.p;
+  p.prof = nullptr;
+  if (a->flags & CTCEXT_FLAG_PHASES) {
+    HIP_OR_FAIL(d->phase.ensure(8 * ctcx::kPhaseN * (size_t)B));
+    p.prof = (uint64_t*)d->phase.p;
+  }
   HIP_OR_FAIL(ctcx::launch_decode<T>(p, s));
   if (prof) HIP_OR_FAIL(hipEventRecord(d->ev[2], s));
 

@@ -43,6 +43,7 @@ constexpr int F_HN = 8;      // has a label-ending alignment candidate
 // per-frame branch state bits
 constexpr int S_EVICT = 1;   // pushed this frame, then evicted from the beam
 constexpr int S_DEACT = 2;   // deactivated (oldp reset): grows no children
+constexpr int kDeactRec = 1 << 30;   // exact_step chunk record: deactivation (else eviction)
 
 template <typename T> __host__ __device__ __forceinline__ T ninf();
 template <> __host__ __device__ __forceinline__ float ninf<float>() { return -__builtin_inff(); }
@@ -71,6 +72,14 @@ __device__ __forceinline__ double bcast(double v, int k) {
 }
 __device__ __forceinline__ int bcast(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
 
+// Wave-uniform values that come out of LDS or VALU: readfirstlane moves them to
+// SGPRs so the loops and branches they control stay scalar (no exec masking).
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ float uni(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
+__device__ __forceinline__ double uni(double v) { return bcast(v, 0); }
+
 template <typename T>
 __device__ __forceinline__ T wave_min(T v) {
 #pragma unroll
@@ -98,25 +107,71 @@ template <typename T> struct HE;
 template <> struct __attribute__((aligned(8))) HE<float> { float v; int s; };
 template <> struct __attribute__((aligned(16))) HE<double> { double v; int s; int pad; };
 
+typedef unsigned u32x2 __attribute__((ext_vector_type(2), may_alias));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4), may_alias));
+
+// Heap element loads/stores as single 8-byte (float) / 16-byte (double) LDS
+// accesses; a pair of siblings is one 16-byte (two for double) access.
+// (vector elements are copied to scalars before __builtin_bit_cast: clang
+// bit-casts an ext-vector element lvalue from element 0's bits)
+__host__ __device__ __forceinline__ HE<float> he_ld(const CTCX_LDS HE<float>* he, int i) {
+  const u32x2 q = *(const CTCX_LDS u32x2*)(he + i);
+  const unsigned x = q.x, y = q.y;
+  return HE<float>{__builtin_bit_cast(float, x), (int)y};
+}
+__host__ __device__ __forceinline__ void he_st(CTCX_LDS HE<float>* he, int i, HE<float> e) {
+  u32x2 q;
+  q.x = __builtin_bit_cast(unsigned, e.v);
+  q.y = (unsigned)e.s;
+  *(CTCX_LDS u32x2*)(he + i) = q;
+}
+__host__ __device__ __forceinline__ void he_ld2(const CTCX_LDS HE<float>* he, int i, HE<float>& a, HE<float>& b) {
+  const u32x4 q = *(const CTCX_LDS u32x4*)(he + i);   // i even: 16-byte aligned
+  const unsigned x = q.x, y = q.y, z = q.z, w = q.w;
+  a = HE<float>{__builtin_bit_cast(float, x), (int)y};
+  b = HE<float>{__builtin_bit_cast(float, z), (int)w};
+}
+__device__ __forceinline__ HE<double> he_ld(const CTCX_LDS HE<double>* he, int i) {
+  const u32x4 q = *(const CTCX_LDS u32x4*)(he + i);
+  const unsigned x = q.x, y = q.y, z = q.z;
+  return HE<double>{__builtin_bit_cast(double, ((uint64_t)y << 32) | x), (int)z, 0};
+}
+__device__ __forceinline__ void he_st(CTCX_LDS HE<double>* he, int i, HE<double> e) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, e.v);
+  u32x4 q;
+  q.x = (unsigned)u; q.y = (unsigned)(u >> 32); q.z = (unsigned)e.s; q.w = 0;
+  *(CTCX_LDS u32x4*)(he + i) = q;
+}
+__device__ __forceinline__ void he_ld2(const CTCX_LDS HE<double>* he, int i, HE<double>& a, HE<double>& b) {
+  a = he_ld(he, i);
+  b = he_ld(he, i + 1);
+}
+
 template <typename T>
 struct Ctx {
   // branch arrays, double-buffered by frame parity: [buf][i]
-  T* ot[2]; T* ob[2]; T* ol[2]; T* cb[2]; T* cn[2];
-  int* lab[2]; int* par[2]; int* flg[2];
-  int* head; int* sib; int* bst; int* newpos;
-  // entries (fast: beam slots; literal: node slots), capacity 2W+2
-  T* et; T* eb; T* el; T* ecb; T* ecn;
-  uint32_t* ebpb; uint32_t* ebpn; uint32_t* ekind; int* elab; int* eflg;
-  int* heap; int* tops; int* freel; int* sorted;
-  T* row;
-  int* misc;
+  CTCX_LDS T* ot[2]; CTCX_LDS T* ob[2]; CTCX_LDS T* ol[2]; CTCX_LDS T* cb[2]; CTCX_LDS T* cn[2];
+  CTCX_LDS int* lab[2]; CTCX_LDS int* par[2]; CTCX_LDS int* flg[2];
+  CTCX_LDS int* head; CTCX_LDS int* sib; CTCX_LDS int* bst; CTCX_LDS int* newpos;
+  // entries (fast: beam slots; literal: node slots), capacity enc = 3W+2
+  CTCX_LDS T* et; CTCX_LDS T* eb; CTCX_LDS T* el; CTCX_LDS T* ecb; CTCX_LDS T* ecn;
+  CTCX_LDS uint32_t* ebpb; CTCX_LDS uint32_t* ebpn; CTCX_LDS uint32_t* ekind;
+  CTCX_LDS int* elab; CTCX_LDS int* eflg;
+  CTCX_LDS int* heap; CTCX_LDS int* tops; CTCX_LDS int* freel; CTCX_LDS int* sorted;
+  CTCX_LDS T* row;
+  CTCX_LDS int* misc;
   // prefix identity: 128-bit hash of each branch's label prefix and of its
   // parent's, [buf][i]; htab maps the hash of a frame's new leaves to position
-  uint64_t* ha[2]; uint64_t* hb[2]; uint64_t* pha[2]; uint64_t* phb[2];
-  int* htab;
-  HE<T>* he;           // TopN elements_, position p at he[p + 1]
+  CTCX_LDS uint64_t* ha[2]; CTCX_LDS uint64_t* hb[2]; CTCX_LDS uint64_t* pha[2]; CTCX_LDS uint64_t* phb[2];
+  CTCX_LDS int* htab;
+  CTCX_LDS HE<T>* he;  // TopN elements_, position p at he[p + 1]
   int W, C, blank, enc, hts;
 };
+
+// Frame-parity buffer select without indexing the pointer pair, so Ctx stays
+// in registers (a runtime index into a member array would force it to scratch).
+template <typename P>
+__host__ __device__ __forceinline__ P sel(P const (&a)[2], int b) { return b ? a[1] : a[0]; }
 
 // Prefix hashing (stands in for the reference's trie, ctc_beam_entry.h:114-122
 // and 248-269): a node's identity is its label prefix; h(prefix + [l]) =
@@ -137,51 +192,51 @@ __host__ __device__ __forceinline__ void hmix(uint64_t a, uint64_t b, int l, uin
 constexpr uint64_t kRootHa = 0x243F6A8885A308D3ull, kRootHb = 0x13198A2E03707344ull;
 
 template <typename T>
-__host__ __device__ void carve(Ctx<T>& cx, char* base, int W, int C) {
-  const size_t ENC = 2 * (size_t)W + 2;
+__host__ __device__ void carve(Ctx<T>& cx, CTCX_LDS char* base, int W, int C) {
+  const size_t ENC = 3 * (size_t)W + 2;
   auto a16 = [](size_t v) { return (v + 15) & ~(size_t)15; };
-  char* p = base;
+  CTCX_LDS char* p = base;
   for (int b = 0; b < 2; ++b) {
-    T* q = (T*)p;
+    CTCX_LDS T* q = (CTCX_LDS T*)p;
     cx.ot[b] = q; cx.ob[b] = q + W; cx.ol[b] = q + 2 * W; cx.cb[b] = q + 3 * W; cx.cn[b] = q + 4 * W;
     p += a16(5 * (size_t)W * sizeof(T));
   }
   for (int b = 0; b < 2; ++b) {
-    int* q = (int*)p;
+    CTCX_LDS int* q = (CTCX_LDS int*)p;
     cx.lab[b] = q; cx.par[b] = q + W; cx.flg[b] = q + 2 * W;
     p += a16(3 * (size_t)W * 4);
   }
   {
-    int* q = (int*)p;
+    CTCX_LDS int* q = (CTCX_LDS int*)p;
     cx.head = q; cx.sib = q + W; cx.bst = q + 2 * W; cx.newpos = q + 3 * W;
     p += a16(4 * (size_t)W * 4);
   }
   {
-    T* q = (T*)p;
+    CTCX_LDS T* q = (CTCX_LDS T*)p;
     cx.et = q; cx.eb = q + ENC; cx.el = q + 2 * ENC; cx.ecb = q + 3 * ENC; cx.ecn = q + 4 * ENC;
     p += a16(5 * ENC * sizeof(T));
   }
   {
-    uint32_t* q = (uint32_t*)p;
+    CTCX_LDS uint32_t* q = (CTCX_LDS uint32_t*)p;
     cx.ebpb = q; cx.ebpn = q + ENC; cx.ekind = q + 2 * ENC;
-    cx.elab = (int*)(q + 3 * ENC); cx.eflg = (int*)(q + 4 * ENC);
+    cx.elab = (CTCX_LDS int*)(q + 3 * ENC); cx.eflg = (CTCX_LDS int*)(q + 4 * ENC);
     p += a16(5 * ENC * 4);
   }
-  cx.heap = (int*)p; p += a16(((size_t)W + 1) * 4);
-  cx.tops = (int*)p; p += a16(((size_t)W + 1) * 4);
-  cx.freel = (int*)p; p += a16(ENC * 4);
-  cx.sorted = (int*)p; p += a16((size_t)W * 4);
-  cx.row = (T*)p; p += a16((size_t)C * sizeof(T));
-  cx.misc = (int*)p; p += 64;
+  cx.heap = (CTCX_LDS int*)p; p += a16(((size_t)W + 1) * 4);
+  cx.tops = (CTCX_LDS int*)p; p += a16(((size_t)W + 1) * 4);
+  cx.freel = (CTCX_LDS int*)p; p += a16(ENC * 4);
+  cx.sorted = (CTCX_LDS int*)p; p += a16((size_t)W * 4);
+  cx.row = (CTCX_LDS T*)p; p += a16((size_t)C * sizeof(T));
+  cx.misc = (CTCX_LDS int*)p; p += 64;
   for (int b = 0; b < 2; ++b) {
-    uint64_t* q = (uint64_t*)p;
+    CTCX_LDS uint64_t* q = (CTCX_LDS uint64_t*)p;
     cx.ha[b] = q; cx.hb[b] = q + W; cx.pha[b] = q + 2 * W; cx.phb[b] = q + 3 * W;
     p += 4 * (size_t)W * 8;
   }
   cx.hts = htab_size(W);
-  cx.htab = (int*)p;
+  cx.htab = (CTCX_LDS int*)p;
   p += a16(4 * (size_t)cx.hts);
-  cx.he = (HE<T>*)p;
+  cx.he = (CTCX_LDS HE<T>*)p;
   cx.W = W; cx.C = C; cx.enc = (int)ENC;
 }
 
@@ -190,9 +245,9 @@ __host__ __device__ void carve(Ctx<T>& cx, char* base, int W, int C) {
 template <typename T>
 __host__ __device__ __forceinline__ void cand_from(const Ctx<T>& cx, int buf, int src, int kind, T p, T restart,
                                           Best<T>& best) {
-  const int f = cx.flg[buf][src];
+  const int f = sel(cx.flg, buf)[src];
   const bool has = (f & (kind == 0 ? F_HB : F_HN)) != 0;
-  const T base = has ? (kind == 0 ? cx.cb[buf][src] : cx.cn[buf][src]) : restart;
+  const T base = has ? (kind == 0 ? sel(cx.cb, buf)[src] : sel(cx.cn, buf)[src]) : restart;
   best.push(base + p, has ? (((uint32_t)src << 1) | (uint32_t)kind) : kBpRestart);
 }
 
@@ -200,12 +255,12 @@ __host__ __device__ __forceinline__ void cand_from(const Ctx<T>& cx, int buf, in
 // arrays and the entry i's current newp (rolled = oldp, except in literal mode
 // where a parent processed earlier may have changed its own entry).
 template <typename T>
-__host__ __device__ void recurse_branch(const Ctx<T>& cx, int buf, int i, T norm, bool literal) {
+__host__ __device__ __forceinline__ void recurse_branch(const Ctx<T>& cx, int buf, int i, T norm, bool literal) {
   const T NI = ninf<T>();
-  const int f = cx.flg[buf][i];
-  const int L = cx.lab[buf][i];
+  const int f = sel(cx.flg, buf)[i];
+  const int L = sel(cx.lab, buf)[i];
   const bool isroot = (f & F_ROOT) != 0;
-  const T o_t = cx.ot[buf][i];
+  const T o_t = sel(cx.ot, buf)[i];
   const bool fresh = (o_t == NI);
   // restart base for a from-blank candidate with receiver i
   const T rs_blank = (isroot || ((f & F_PROOT) && fresh)) ? T(0) : NI;
@@ -214,11 +269,11 @@ __host__ __device__ void recurse_branch(const Ctx<T>& cx, int buf, int i, T norm
   if (!isroot) {
     const T xl = cx.row[L];
     const T p = xl - norm;
-    const int P = cx.par[buf][i];
+    const int P = sel(cx.par, buf)[i];
     const bool pactive = (P >= 0) && (!literal || cx.et[P] != NI);
     if (pactive) {
-      const bool same = (L == cx.lab[buf][P]);
-      const T prev = same ? cx.ob[buf][P] : cx.ot[buf][P];
+      const bool same = (L == sel(cx.lab, buf)[P]);
+      const T prev = same ? sel(cx.ob, buf)[P] : sel(cx.ot, buf)[P];
       nl = lse(nl, prev) + xl - norm;
       cand_from(cx, buf, P, 0, p, rs_blank, bn);
       if (!same) cand_from(cx, buf, P, 1, p, NI, bn);
@@ -259,112 +314,165 @@ __host__ __device__ void recurse_branch(const Ctx<T>& cx, int buf, int i, T norm
 
 // libstdc++ __adjust_heap + __push_heap, one lane, on positions [0, len).
 template <typename T>
-__device__ void lane_adjust_heap(HE<T>* he, int hole, int len, HE<T> value) {
+__host__ __device__ void lane_adjust_heap(CTCX_LDS HE<T>* he, int hole, int len, HE<T> value) {
   const int top = hole;
   int second = hole;
   while (second < (len - 1) / 2) {
     second = 2 * (second + 1);
-    if (he[second + 1].v > he[second].v) second--;
-    he[hole + 1] = he[second + 1];
+    HE<T> l, r;
+    he_ld2(he, second, l, r);          // positions second-1, second
+    if (r.v > l.v) { second--; r = l; }
+    he_st(he, hole + 1, r);
     hole = second;
   }
   if ((len & 1) == 0 && second == (len - 2) / 2) {
     second = 2 * (second + 1);
-    he[hole + 1] = he[second];
+    he_st(he, hole + 1, he_ld(he, second));
     hole = second - 1;
   }
   int parent = (hole - 1) / 2;
-  while (hole > top && he[parent + 1].v > value.v) {
-    he[hole + 1] = he[parent + 1];
+  while (hole > top) {
+    const HE<T> pe = he_ld(he, parent + 1);
+    if (!(pe.v > value.v)) break;
+    he_st(he, hole + 1, pe);
     hole = parent;
     parent = (hole - 1) / 2;
   }
-  he[hole + 1] = value;
+  he_st(he, hole + 1, value);
 }
 
 // std::make_heap over [0, len).  Parents at one depth own disjoint subtrees,
 // so each level's sift-downs run in parallel lanes (deepest level first, the
 // order libstdc++ visits them in).
 template <typename T>
-__device__ void wave_make_heap(HE<T>* he, int len) {
+__device__ void wave_make_heap(CTCX_LDS HE<T>* he, int len) {
   if (len < 2) return;
   const int last = (len - 2) / 2;
   const int dmax = 31 - __builtin_clz((unsigned)(last + 1));
   for (int d = dmax; d >= 0; --d) {
     const int lo = (1 << d) - 1;
     const int hi = min((1 << (d + 1)) - 2, last);
-    for (int i = lo + (int)threadIdx.x; i <= hi; i += 64) lane_adjust_heap(he, i, len, he[i + 1]);
+    for (int i = lo + (int)threadIdx.x; i <= hi; i += 64) lane_adjust_heap(he, i, len, he_ld(he, i + 1));
   }
 }
 
-// __adjust_heap(top, len, v) for the whole wave.  The hole descends along the
+// __adjust_heap(0, len, v) for the whole wave.  The hole descends along the
 // smaller child (right on ties) to a leaf and v then rises while its parent is
-// strictly greater; since values along that path are non-decreasing this is
-// "walk the min-child path while the child is <= v".  Every lane computes the
-// min child of its internal nodes in parallel (one LDS pair read each); the
-// walk is a uniform readlane chase.  Requires finite values below `top`.
+// strictly greater; since values along that path are non-decreasing, v stops
+// at the first node of the root's min-child path whose min child is > v (or
+// whose min child is a leaf, which v then takes), and every path node above
+// the stop takes its min child.  A single wave pays a pipeline round trip for
+// every VALU -> scalar hand-off, so the path is found lane-parallel instead of
+// by walking it: every lane loads the child pair of its node(s) (one LDS
+// batch), one ballot gives the min-child directions of all nodes, each lane
+// checks in integer arithmetic that every ancestor of its node points toward
+// it (its node is then on the path), and a second ballot + find-first-set
+// yields the stop.  All writes are one parallel store.  If vpos >= 0 v is read
+// from position vpos in the same LDS batch (pop_heap).  Returns the new root;
+// v, the result and all other uniform values stay in VGPRs.
 template <typename T, int RN>
-__device__ void wave_adjust_heap(HE<T>* he, int top, int len, HE<T> v) {
+__device__ __forceinline__ HE<T> wave_adjust_heap(CTCX_LDS HE<T>* he, int len, HE<T> v, int vpos = -1) {
+  constexpr int KMAX = 6 + (RN >= 2 ? 1 : 0) + (RN >= 4 ? 1 : 0);   // depth bound of a lane node
   const int lane = threadIdx.x;
+  len = uni(len);
   const int nint = len / 2;   // nodes with at least one child
-  int nx[RN];
+  const int imax = nint > 0 ? nint - 1 : 0;
+  if (vpos >= 0) v = he_ld(he, uni(vpos) + 1);
+  HE<T> L[RN], R[RN];
+#pragma unroll
+  for (int r = 0; r < RN; ++r) he_ld2(he, 2 * min(r * 64 + lane, imax) + 2, L[r], R[r]);
   T cv[RN];
   int cs[RN];
+  unsigned pk[RN];
+  uint64_t bm[RN];
 #pragma unroll
   for (int r = 0; r < RN; ++r) {
-    const int i = r * 64 + lane;
-    nx[r] = -1; cv[r] = T(0); cs[r] = 0;
-    if (i < nint && i >= top) {
-      const HE<T> L = he[2 * i + 2];
-      int c = 2 * i + 1;
-      HE<T> ch = L;
-      if (2 * i + 2 < len) {
-        const HE<T> Rt = he[2 * i + 3];
-        if (!(Rt.v > L.v)) { c = 2 * i + 2; ch = Rt; }
+    const int i = min(r * 64 + lane, imax);
+    const bool pick_r = (2 * i + 2 < len) && !(R[r].v > L[r].v);
+    bm[r] = __ballot(pick_r);
+    pk[r] = pick_r ? 1u : 0u;
+    cv[r] = pick_r ? R[r].v : L[r].v;
+    cs[r] = pick_r ? R[r].s : L[r].s;
+  }
+  const T c0 = bcast(cv[0], 0);
+  const int s0 = bcast(cs[0], 0);
+  uint64_t cm[RN];
+  unsigned offp[RN], gtv[RN];
+#pragma unroll
+  for (int r = 0; r < RN; ++r) {
+    const unsigned j = (unsigned)(r * 64 + lane);
+    const unsigned J = j + 1u;
+    const int dj = 31 - __builtin_clz(J);
+    unsigned mis = 0;   // bit k-1: the depth-(dj-k) ancestor's min child is not toward j
+#pragma unroll
+    for (int k = 1; k <= KMAX; ++k) {
+      const unsigned pos = (J >> k) - 1u;   // wraps past the root: masked by dj below
+      unsigned have;
+      if (RN == 1) {
+        have = (unsigned)bm[0] >> (pos & 31u);   // ancestors of nodes < 64 are < 32
+      } else {
+        uint64_t w = bm[0];
+#pragma unroll
+        for (int rr = 1; rr < RN / 2; ++rr) w = ((pos >> 6) == (unsigned)rr) ? bm[rr] : w;
+        have = (unsigned)(w >> (pos & 63u));
       }
-      nx[r] = c; cv[r] = ch.v; cs[r] = ch.s;
+      mis |= ((have ^ (J >> (k - 1))) & 1u) << (k - 1);
+    }
+    mis &= (1u << dj) - 1u;
+    offp[r] = mis | (j >= (unsigned)nint ? 1u : 0u);
+    gtv[r] = (cv[r] > v.v) ? 1u : 0u;
+    const unsigned leaf = (2u * j + 1u + pk[r] >= (unsigned)nint) ? 1u : 0u;
+    cm[r] = __ballot((offp[r] | ((gtv[r] | leaf) ^ 1u)) == 0u);
+  }
+  int kk = -1;
+#pragma unroll
+  for (int r = RN - 1; r >= 0; --r)
+    if (cm[r]) kk = r * 64 + (int)__builtin_ctzll(cm[r]);
+  if (kk < 0) {
+    if (lane == 0) he_st(he, 1, v);
+  } else {
+#pragma unroll
+    for (int r = 0; r < RN; ++r) {
+      const int j = r * 64 + lane;
+      if (offp[r] == 0u && (j < kk || (j == kk && gtv[r] == 0u))) he_st(he, j + 1, HE<T>{cv[r], cs[r]});
+      if (j == kk) he_st(he, (gtv[r] ? j : 2 * j + 1 + (int)pk[r]) + 1, v);
     }
   }
-  int p = top;
-  while (p < nint) {
-    const int rr = p >> 6, l = p & 63;
-    int q = nx[0];
-    T a = cv[0];
-    int sl = cs[0];
-#pragma unroll
-    for (int r = 1; r < RN; ++r)
-      if (rr == r) { q = nx[r]; a = cv[r]; sl = cs[r]; }
-    q = bcast(q, l);
-    a = bcast(a, l);
-    sl = bcast(sl, l);
-    if (a > v.v) break;
-    if (lane == 0) he[p + 1] = HE<T>{a, sl};
-    p = q;
-  }
-  if (lane == 0) he[p + 1] = v;
+  HE<T> res;
+  const bool keep = (nint == 0) || (c0 > v.v);
+  res.v = keep ? v.v : c0;
+  res.s = keep ? v.s : s0;
+  return res;
 }
 
 // peek_bottom() in the UNORDERED state: the first minimum moves to the front.
+// Returns the new front.
 template <typename T>
-__device__ void wave_first_min_to_front(HE<T>* he, int n) {
+__device__ HE<T> wave_first_min_to_front(CTCX_LDS HE<T>* he, int n) {
   const int lane = threadIdx.x;
   T mv = pinf<T>();
-  int mi = 0x7fffffff;
+  int mi = 0x7fffffff, ms = 0;
   for (int i = lane; i < n; i += 64) {
-    const T v = he[i + 1].v;
-    if (v < mv) { mv = v; mi = i; }
+    const HE<T> e = he_ld(he, i + 1);
+    if (e.v < mv) { mv = e.v; mi = i; ms = e.s; }
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
     const T ov = __shfl_xor(mv, o);
     const int oi = __shfl_xor(mi, o);
-    if (ov < mv || (ov == mv && oi < mi)) { mv = ov; mi = oi; }
+    const int os = __shfl_xor(ms, o);
+    if (ov < mv || (ov == mv && oi < mi)) { mv = ov; mi = oi; ms = os; }
   }
+  mi = uni(mi);
   if (mi != 0 && lane == 0) {
-    const HE<T> a = he[1];
-    he[1] = he[mi + 1];
-    he[mi + 1] = a;
+    const HE<T> a = he_ld(he, 1);
+    he_st(he, 1, he_ld(he, mi + 1));
+    he_st(he, mi + 1, a);
   }
+  HE<T> f;
+  f.v = uni(mv);
+  f.s = uni(ms);
+  return f;
 }
 
 // ---------------------------------------------------------------------------
@@ -377,14 +485,15 @@ __device__ void wave_first_min_to_front(HE<T>* he, int n) {
 // On success cx.sorted[0..*n_out) holds the Extract() order and, for the last
 // frame, cx.tops[0..min(P, leaves)) the TopPaths() selection as positions.
 template <typename T, int RN>
-__device__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, bool last, int P, int* n_out,
-                          int* n_leaves) {
+__device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, bool last, int P, int* n_out,
+                          int* n_leaves, uint64_t* pc) {
+  uint64_t ts0 = pc ? __builtin_amdgcn_s_memtime() : 0;
   const int lane = threadIdx.x;
   const T NI = ninf<T>();
   const int W = cx.W;
   const int C = cx.C;
   const int blank = cx.blank;
-  HE<T>* he = cx.he;
+  CTCX_LDS HE<T>* he = cx.he;
 
   bool bad = !(norm > NI && norm < pinf<T>());
   for (int j = lane; j < C; j += 64) {
@@ -395,7 +504,7 @@ __device__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, bool last, int P,
 
   // roll (decoder.h:87-92) + recursion (decoder.h:95-143), lanes over branches
   for (int i = lane; i < nb; i += 64) {
-    cx.et[i] = cx.ot[buf][i]; cx.eb[i] = cx.ob[buf][i]; cx.el[i] = cx.ol[buf][i];
+    cx.et[i] = sel(cx.ot, buf)[i]; cx.eb[i] = sel(cx.ob, buf)[i]; cx.el[i] = sel(cx.ol, buf)[i];
     cx.eflg[i] = 0;
     cx.bst[i] = 0;
   }
@@ -406,126 +515,154 @@ __device__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, bool last, int P,
   for (int i = lane; i < nb; i += 64) {
     const T v = cx.et[i];
     nonfinite |= !(v > NI && v < pinf<T>());
-    he[i + 1] = HE<T>{v, i};           // leaves_.push(b) in branch order
+    he_st(he, i + 1, HE<T>{v, i});     // leaves_.push(b) in branch order
   }
-  for (int k = lane; k < cx.enc - nb; k += 64) cx.freel[k] = nb + k;
   if (__ballot(nonfinite)) return 1;
   __syncthreads();
 
+  uint64_t ts1 = pc ? __builtin_amdgcn_s_memtime() : 0;
+  if (pc) pc[1] += ts1 - ts0;
   int n = nb;                     // elements_.size()
-  int nfree = cx.enc - nb;
+  // Child slots come from a bump allocator; a new child reuses the slot of the
+  // child entry it evicts.  A bump happens for an append before the beam is
+  // full (<= W - nb) or when the evicted entry is a branch's (a branch is
+  // evicted at most twice: it re-enters only through its one (parent, label)
+  // offer), so slots stay below W + 2 nb <= 3W < enc.
+  int nextfree = nb;
   int st = kTopUnordered;
   bool full = (n >= W);
+  HE<T> front;                    // elements_[0] once BOTTOM_KNOWN / HEAP (uniform, in VGPRs)
+  front.v = NI;
+  front.s = 0;
   if (full) {                     // branch 0's is_candidate() peeks
-    wave_first_min_to_front(he, n);
+    front = wave_first_min_to_front(he, n);
     st = kTopBottomKnown;
   }
-  T bottom = full ? he[1].v : NI;
+  T bottom = full ? front.v : NI;
 
-  // grow (decoder.h:146-209): offers in (branch order, label order)
+  // grow (decoder.h:146-209): offers in (branch order, label order), 64 per
+  // chunk.  Within a chunk the entry writes, the resets of evicted branch
+  // entries and the S_EVICT / S_DEACT flags are kept in registers (myslot, the
+  // record list evr/nev) and flushed by all lanes at the chunk's end: nothing
+  // reads them before then, and an event then costs no divergent stores.
   const int Cm1 = C - 1;
   const int64_t total = (int64_t)nb * Cm1;
   for (int64_t f0 = 0; f0 < total; f0 += 64) {
     const int i0 = (int)(f0 / Cm1);
-    if (full && !(cx.ot[buf][i0] > bottom)) break;   // every later branch is skipped
+    if (full && uni((int)!(sel(cx.ot, buf)[i0] > bottom))) break;   // every later branch is skipped
+    const uint64_t tc0 = pc ? __builtin_amdgcn_s_memtime() : 0;
     const int64_t f = f0 + lane;
     const bool valid = f < total;
     const int i = valid ? (int)(f / Cm1) : i0;
     const int li = valid ? (int)(f - (int64_t)i * Cm1) : 0;
     const int l = li + (li >= blank ? 1 : 0);
-    const int bl = cx.lab[buf][i];
-    const int bflg = cx.flg[buf][i];
-    const T bt = cx.ot[buf][i];
+    const int bl = sel(cx.lab, buf)[i];
+    const int bflg = sel(cx.flg, buf)[i];
+    const T bt = sel(cx.ot, buf)[i];
     bool live = valid && !(cx.bst[i] & S_DEACT);
     const T xl = cx.row[l];
     const T p = xl - norm;
-    const T s = p + ((l == bl) ? cx.ob[buf][i] : bt);
+    const T s = p + ((l == bl) ? sel(cx.ob, buf)[i] : bt);
     int c = -1;
     if (live) {
       for (int k = cx.head[i]; k >= 0; k = cx.sib[k])
-        if (cx.lab[buf][k] == l) { c = k; break; }
+        if (sel(cx.lab, buf)[k] == l) { c = k; break; }
     }
     const bool isbc = c >= 0;
     bool cev = isbc && (cx.bst[c] & S_EVICT);
     // label-ending candidate for the child (decoder.h:172-185)
-    const bool recv_fresh = isbc ? (cx.ot[buf][c] == NI) : true;
+    const bool recv_fresh = isbc ? (sel(cx.ot, buf)[c] == NI) : true;
     const T rs_blank = ((bflg & F_ROOT) && recv_fresh) ? T(0) : NI;
     Best<T> cd{T(0), kBpNone, false};
     cand_from(cx, buf, i, 0, p, rs_blank, cd);
     if (l != bl) cand_from(cx, buf, i, 1, p, NI, cd);
+    const uint64_t isbm = __ballot(isbc);
 
+    uint64_t tc1 = pc ? __builtin_amdgcn_s_memtime() : 0;
+    if (pc) { pc[8] += tc1 - tc0; pc[11] += 1; }
+    int myslot = -1;   // slot of this lane's accepted offer (-1: none, or evicted again)
+    int evr = 0;       // record nev-th: evicted branch slot, or kDeactRec | rejected branch
+    int nev = 0;
     uint64_t done = 0;
     while (true) {
       const bool want = live && (isbc ? cev : (s > (full ? bottom : NI)));
+      const bool acc = !isbc || (s > NI && (!full || s > bottom));
       const uint64_t m = __ballot(want) & ~done;
       if (m == 0) break;
       const int k = __ffsll((unsigned long long)m) - 1;
       done = (k == 63) ? ~0ull : ((2ull << k) - 1ull);
-      const int k_isbc = bcast((int)isbc, k);
+      const bool k_isbc = (isbm >> k) & 1ull;
+      const bool accept = (__ballot(acc) >> k) & 1ull;
       const int k_c = bcast(c, k);
-      const T k_s = bcast(s, k);
-      const bool accept = k_isbc ? (k_s > NI && (!full || k_s > bottom)) : true;
+      if (pc) pc[6] += 1;
       if (accept) {
-        int slot;
-        if (k_isbc) {
-          slot = k_c;
-        } else {
-          slot = cx.freel[nfree - 1];
-          --nfree;
-        }
-        if (full) {
-          // evict the bottom (decoder.h:192-198): it is the front
-          const int fslot = he[1].s;
-          if (lane == 0) {
-            cx.et[fslot] = NI; cx.eb[fslot] = NI; cx.el[fslot] = NI; cx.eflg[fslot] = 0;
-            he[1].v = NI;
-          }
-          if (fslot < nb) {
-            if (lane == 0) cx.bst[fslot] |= S_EVICT;
-            if (isbc && c == fslot) cev = true;
-          } else {
-            if (lane == 0) cx.freel[nfree] = fslot;
-            ++nfree;
-          }
-        }
-        if (lane == k) {
-          cx.et[slot] = s; cx.eb[slot] = NI; cx.el[slot] = s;
-          cx.ecn[slot] = cd.p; cx.ebpn[slot] = cd.bp;
-          cx.eflg[slot] = F_HN;
-          cx.ekind[slot] = isbc ? ((uint32_t)c << 1) : (((uint32_t)i << 1) | 1u);
-          cx.elab[slot] = l;
-          if (isbc) cx.bst[c] &= ~S_EVICT;
-        }
-        const HE<T> nv{k_s, slot};
+        if (pc) pc[12] += 1;
+        const T k_s = bcast(s, k);
+        // the evicted bottom is the front (decoder.h:192-198)
+        const int fsl = front.s;
+        const bool evb = full && fsl < nb;   // a branch's entry: reset, flagged
+        const bool evc = full && fsl >= nb;  // a new child's entry: its slot is reused
+        const int slot = k_isbc ? k_c : (evc ? fsl : nextfree);
+        nextfree += (!k_isbc && !evc) ? 1 : 0;
+        myslot = (full && myslot == fsl) ? -1 : myslot;
+        evr = (evb && lane == nev) ? fsl : evr;
+        nev += evb ? 1 : 0;
+        myslot = (lane == k) ? slot : myslot;
+        cev = cev || (evb && isbc && c == fsl);
+        HE<T> nv;
+        nv.v = k_s;
+        nv.s = slot;
         if (st == kTopHeap) {
-          wave_adjust_heap<T, RN>(he, 0, W, nv);          // push = pop_heap(W + 1)
+          uint64_t th0 = pc ? __builtin_amdgcn_s_memtime() : 0;
+          front = wave_adjust_heap<T, RN>(he, W, nv);   // push = pop_heap(W + 1)
+          if (pc) { pc[10] += __builtin_amdgcn_s_memtime() - th0; pc[13] += 1; }
         } else {
-          if (lane == 0) he[n + 1] = nv;
+          // UNORDERED (not full) appends; BOTTOM_KNOWN only ever sees a push right
+          // after its front was evicted (-inf), so the swap check never fires
+          if (full && lane == 0) he[1].v = NI;
+          if (lane == 0) he_st(he, n + 1, nv);
           ++n;
-          if (st == kTopBottomKnown && !(k_s > he[1].v) && lane == 0) {
-            const HE<T> a = he[1];
-            he[1] = he[n];
-            he[n] = a;
-          }
           if (n == W + 1) {
             wave_make_heap(he, W + 1);
-            const HE<T> v2 = he[W + 1];
-            if (lane == 0) he[W + 1] = he[1];
-            wave_adjust_heap<T, RN>(he, 0, W, v2);
+            const HE<T> r0 = he_ld(he, 1);
+            front = wave_adjust_heap<T, RN>(he, W, nv, W);   // pop_heap(W + 1)
+            if (lane == 0) he_st(he, W + 1, r0);
             st = kTopHeap;
           } else if (n == W) {
             return 2;   // filled mid-frame: the lazy peek is replayed literally
           }
         }
-        if (full) bottom = he[1].v;
+        if (full) bottom = front.v;
       } else {
         // re-offered evicted branch rejected -> deactivated (decoder.h:200-205)
-        if (lane == 0) cx.bst[k_c] |= S_DEACT;
-        if (i == k_c) live = false;
+        evr = (lane == nev) ? (k_c | kDeactRec) : evr;
+        nev += 1;
+        live = live && (i != k_c);
       }
     }
+    // flush: resets and flags first, then the surviving accepted entries
+    if (lane < nev) {
+      const int rs = evr & ~kDeactRec;
+      if (evr & kDeactRec) {
+        __hip_atomic_fetch_or(&cx.bst[rs], S_DEACT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else {
+        cx.et[rs] = NI; cx.eb[rs] = NI; cx.el[rs] = NI; cx.eflg[rs] = 0;
+        __hip_atomic_fetch_or(&cx.bst[rs], S_EVICT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    if (myslot >= 0) {
+      cx.et[myslot] = s; cx.eb[myslot] = NI; cx.el[myslot] = s;
+      cx.ecn[myslot] = cd.p; cx.ebpn[myslot] = cd.bp;
+      cx.eflg[myslot] = F_HN;
+      cx.ekind[myslot] = isbc ? ((uint32_t)c << 1) : (((uint32_t)i << 1) | 1u);
+      cx.elab[myslot] = l;
+      if (isbc) __hip_atomic_fetch_and(&cx.bst[c], ~S_EVICT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (pc) pc[9] += __builtin_amdgcn_s_memtime() - tc1;
   }
 
+  uint64_t ts2 = pc ? __builtin_amdgcn_s_memtime() : 0;
+  if (pc) pc[2] += ts2 - ts1;
   const int size = n < W ? n : W;
   *n_leaves = size;
   // TopPaths (decoder.h:245-252) reads the unsorted layout: lane 0, literal
@@ -543,10 +680,11 @@ __device__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, bool last, int P,
   // Extract() of the next frame (decoder.h:84): sort_heap, or std::sort
   int nout;
   if (st == kTopHeap) {
+    // pop_heap(len): e[len-1] <- e[0], then sift the old e[len-1] from the root
     for (int len = W; len > 1; --len) {
-      const HE<T> v = he[len];
-      if (lane == 0) he[len] = he[1];
-      wave_adjust_heap<T, RN>(he, 0, len - 1, v);
+      const HE<T> old_front = front;
+      front = wave_adjust_heap<T, RN>(he, len - 1, front, len - 1);
+      if (lane == 0) he_st(he, len, old_front);
     }
     nout = W;
     for (int k = lane; k < nout; k += 64) cx.sorted[k] = he[k + 1].s;
@@ -565,6 +703,7 @@ __device__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, bool last, int P,
     for (int q = 0; q < lim; ++q) cx.tops[q] = cx.freel[cx.tops[q]];
   }
   __syncthreads();
+  if (pc) pc[3] += __builtin_amdgcn_s_memtime() - ts2;
   *n_out = nout;
   return 0;
 }
@@ -575,12 +714,12 @@ __device__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, bool last, int P,
 // (sorted slots in cx.sorted); for the last frame also fills cx.tops[0..P)
 // with the TopPaths selection as slots.  *err = 1 on a duplicate-beam state.
 template <typename T>
-__host__ __device__ int literal_step(Ctx<T>& cx, int buf, int nb, T norm, bool last, int P, int* err,
+__host__ __device__ __attribute__((noinline)) int literal_step(Ctx<T> cx, int buf, int nb, T norm, bool last, int P, int* err,
                             int* n_leaves) {
   const T NI = ninf<T>();
   const int W = cx.W, C = cx.C, blank = cx.blank;
   for (int i = 0; i < nb; ++i) {
-    cx.et[i] = cx.ot[buf][i]; cx.eb[i] = cx.ob[buf][i]; cx.el[i] = cx.ol[buf][i];
+    cx.et[i] = sel(cx.ot, buf)[i]; cx.eb[i] = sel(cx.ob, buf)[i]; cx.el[i] = sel(cx.ol, buf)[i];
     cx.eflg[i] = 0;
     cx.bst[i] = 0;
   }
@@ -596,16 +735,16 @@ __host__ __device__ int literal_step(Ctx<T>& cx, int buf, int nb, T norm, bool l
 
   for (int i = 0; i < nb; ++i) {
     {
-      const T bt = cx.ot[buf][i];
+      const T bt = sel(cx.ot, buf)[i];
       if (!(bt > NI && (h.size() < W || bt > cx.et[lit_top_peek_bottom(h, gt)]))) continue;
     }
-    const int bl = cx.lab[buf][i];
-    const int bflg = cx.flg[buf][i];
+    const int bl = sel(cx.lab, buf)[i];
+    const int bflg = sel(cx.flg, buf)[i];
     for (int l = 0; l < C; ++l) {
       if (l == blank) continue;
       int c = -1;
       for (int k = cx.head[i]; k >= 0; k = cx.sib[k])
-        if (cx.lab[buf][k] == l) { c = k; break; }
+        if (sel(cx.lab, buf)[k] == l) { c = k; break; }
       int slot;
       const bool fresh_slot = (c < 0);
       if (!fresh_slot) {
@@ -618,9 +757,9 @@ __host__ __device__ int literal_step(Ctx<T>& cx, int buf, int nb, T norm, bool l
       const T xl = cx.row[l];
       const T p = xl - norm;
       cx.eb[slot] = NI;
-      const T prev = (l == bl) ? cx.ob[buf][i] : cx.ot[buf][i];
+      const T prev = (l == bl) ? sel(cx.ob, buf)[i] : sel(cx.ot, buf)[i];
       cx.el[slot] = xl - norm + prev;
-      const bool recv_fresh = fresh_slot ? true : (cx.ot[buf][c] == NI);
+      const bool recv_fresh = fresh_slot ? true : (sel(cx.ot, buf)[c] == NI);
       const T rs_blank = ((bflg & F_ROOT) && recv_fresh) ? T(0) : NI;
       Best<T> cd{cx.ecn[slot], cx.ebpn[slot], (cx.eflg[slot] & F_HN) != 0};
       cand_from(cx, buf, i, 0, p, rs_blank, cd);
@@ -644,8 +783,8 @@ __host__ __device__ int literal_step(Ctx<T>& cx, int buf, int nb, T norm, bool l
         cx.et[slot] = NI; cx.eb[slot] = NI; cx.el[slot] = NI;
         cx.eflg[slot] = 0;
         if (!fresh_slot) {
-          cx.ot[buf][c] = NI; cx.ob[buf][c] = NI; cx.ol[buf][c] = NI;
-          cx.flg[buf][c] &= ~(F_HB | F_HN);
+          sel(cx.ot, buf)[c] = NI; sel(cx.ob, buf)[c] = NI; sel(cx.ol, buf)[c] = NI;
+          sel(cx.flg, buf)[c] &= ~(F_HB | F_HN);
         }
       }
     }
@@ -679,7 +818,7 @@ template <typename T, int RN>
 __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   Ctx<T> cx;
-  carve(cx, lds, prm.W, (int)prm.C);
+  carve(cx, (CTCX_LDS char*)lds, prm.W, (int)prm.C);
   cx.blank = prm.blank;
   const int lane = threadIdx.x;
   const int64_t b = blockIdx.x;
@@ -687,7 +826,7 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
   const int C = (int)prm.C;
   const int64_t B = prm.B;
   const int sl = prm.seq_len[b] > 0 ? prm.seq_len[b] : 0;
-  int* const misc = cx.misc;
+  CTCX_LDS int* const misc = cx.misc;
 
   // Reset(): root with newp.total = newp.blank = 0 (decoder.h:213-227)
   int buf = 0;
@@ -705,7 +844,10 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
   int n_leaves = 1;
   __syncthreads();
 
+  uint64_t pc[kPhaseN] = {};
+  const bool prof = prm.prof != nullptr;
   for (int t = 0; t < sl; ++t) {
+    uint64_t t0 = prof ? __builtin_amdgcn_s_memtime() : 0;
     const T* xr = prm.x + ((int64_t)t * B + b) * C;
     for (int j = lane; j < C; j += 64) cx.row[j] = xr[j];
     const T norm = prm.norm[(int64_t)t * B + b];
@@ -715,8 +857,11 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     int n = 0;
     int why = 4;
     int nl_fast = 0;
-    if (!prm.force_literal) why = exact_step<T, RN>(cx, buf, nb, norm, last, prm.P, &n, &nl_fast);
+    uint64_t t1 = prof ? __builtin_amdgcn_s_memtime() : 0;
+    if (prof) pc[0] += t1 - t0;
+    if (!prm.force_literal) why = exact_step<T, RN>(cx, buf, nb, norm, last, prm.P, &n, &nl_fast, prof ? pc : nullptr);
     __syncthreads();
+    uint64_t t2 = prof ? __builtin_amdgcn_s_memtime() : 0;
     const bool ok = (why == 0);
     why_nf += (why == 1); why_et += (why == 2);
     if (!ok) {
@@ -735,6 +880,8 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
       n_leaves = nl_fast;
     }
     __syncthreads();
+    uint64_t t3 = prof ? __builtin_amdgcn_s_memtime() : 0;
+    if (prof) pc[5] += t3 - t2;
 
     // ---- commit: records + next frame's branch arrays (sorted order) ----
     const int nx = buf ^ 1;
@@ -752,15 +899,20 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
       const int src = (int)(kd >> 1);
       uint64_t ha, hb, pa, pb;
       if (kd & 1u) {
-        pa = cx.ha[buf][src]; pb = cx.hb[buf][src];
+        pa = sel(cx.ha, buf)[src]; pb = sel(cx.hb, buf)[src];
         hmix(pa, pb, cx.elab[cx.sorted[k]], ha, hb);
         int q = (int)(ha & (uint64_t)(cx.hts - 1));
-        while (atomicCAS(&cx.htab[q], -1, k) != -1) q = (q + 1) & (cx.hts - 1);
+        int expect = -1;
+        while (!__hip_atomic_compare_exchange_strong(&cx.htab[q], &expect, k, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+          q = (q + 1) & (cx.hts - 1);
+          expect = -1;
+        }
       } else {
-        ha = cx.ha[buf][src]; hb = cx.hb[buf][src];
-        pa = cx.pha[buf][src]; pb = cx.phb[buf][src];
+        ha = sel(cx.ha, buf)[src]; hb = sel(cx.hb, buf)[src];
+        pa = sel(cx.pha, buf)[src]; pb = sel(cx.phb, buf)[src];
       }
-      cx.ha[nx][k] = ha; cx.hb[nx][k] = hb; cx.pha[nx][k] = pa; cx.phb[nx][k] = pb;
+      sel(cx.ha, nx)[k] = ha; sel(cx.hb, nx)[k] = hb; sel(cx.pha, nx)[k] = pa; sel(cx.phb, nx)[k] = pb;
     }
     __syncthreads();
     Rec* rout = prm.rec + ((int64_t)b * prm.Tmax + t) * W;
@@ -769,33 +921,33 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
       const uint32_t kd = cx.ekind[e];
       const int src = (int)(kd >> 1);
       const bool isnew = (kd & 1u) != 0;
-      const int pf = cx.flg[buf][src];
+      const int pf = sel(cx.flg, buf)[src];
       int parent, fl;
       if (isnew) {
         parent = cx.newpos[src];
         fl = (pf & F_ROOT) ? F_PROOT : 0;
       } else {
-        const int pp = cx.par[buf][src];
+        const int pp = sel(cx.par, buf)[src];
         parent = pp >= 0 ? cx.newpos[pp] : -1;
         fl = pf & (F_ROOT | F_PROOT);
         if (pp < 0 && !(pf & F_ROOT)) {
           // the parent node was not in the beam; it may have re-entered this
           // frame as a new child (the reference finds it through the trie)
-          const uint64_t pa = cx.pha[nx][k], pb = cx.phb[nx][k];
+          const uint64_t pa = sel(cx.pha, nx)[k], pb = sel(cx.phb, nx)[k];
           for (int q = (int)(pa & (uint64_t)(cx.hts - 1));; q = (q + 1) & (cx.hts - 1)) {
             const int c = cx.htab[q];
             if (c < 0) break;
-            if (cx.ha[nx][c] == pa && cx.hb[nx][c] == pb) { parent = c; break; }
+            if (sel(cx.ha, nx)[c] == pa && sel(cx.hb, nx)[c] == pb) { parent = c; break; }
           }
         }
       }
       const int ef = cx.eflg[e];
       fl |= ef & (F_HB | F_HN);
-      cx.lab[nx][k] = cx.elab[e];
-      cx.par[nx][k] = parent;
-      cx.flg[nx][k] = fl;
-      cx.ot[nx][k] = cx.et[e]; cx.ob[nx][k] = cx.eb[e]; cx.ol[nx][k] = cx.el[e];
-      cx.cb[nx][k] = cx.ecb[e]; cx.cn[nx][k] = cx.ecn[e];
+      sel(cx.lab, nx)[k] = cx.elab[e];
+      sel(cx.par, nx)[k] = parent;
+      sel(cx.flg, nx)[k] = fl;
+      sel(cx.ot, nx)[k] = cx.et[e]; sel(cx.ob, nx)[k] = cx.eb[e]; sel(cx.ol, nx)[k] = cx.el[e];
+      sel(cx.cb, nx)[k] = cx.ecb[e]; sel(cx.cn, nx)[k] = cx.ecn[e];
       Rec rc;
       rc.link = kd;
       rc.label = cx.elab[e];
@@ -809,11 +961,15 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     for (int k = lane; k < nb; k += 64) cx.head[k] = -1;
     __syncthreads();
     for (int k = lane; k < nb; k += 64) {
-      const int pp = cx.par[buf][k];
-      if (pp >= 0) cx.sib[k] = atomicExch(&cx.head[pp], k);
+      const int pp = sel(cx.par, buf)[k];
+      if (pp >= 0)
+        cx.sib[k] = __hip_atomic_exchange(&cx.head[pp], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     __syncthreads();
+    if (prof) { pc[4] += __builtin_amdgcn_s_memtime() - t3; pc[7] += 1; }
   }
+  if (prof && lane == 0)
+    for (int q = 0; q < kPhaseN; ++q) prm.prof[b * kPhaseN + q] = pc[q];
 
   // TopPaths outputs (decoder.h:230-261); with no frames the root is the leaf
   if (sl == 0 && lane == 0) cx.tops[0] = 0;
@@ -824,12 +980,12 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     T lp = T(0);
     if (q < np) {
       pos = cx.tops[q];
-      const int f = cx.flg[buf][pos];
+      const int f = sel(cx.flg, buf)[pos];
       const bool hb = f & F_HB, hn = f & F_HN;
-      if (hb && hn) kind = (cx.cb[buf][pos] > cx.cn[buf][pos]) ? 0 : 1;
+      if (hb && hn) kind = (sel(cx.cb, buf)[pos] > sel(cx.cn, buf)[pos]) ? 0 : 1;
       else if (hb) kind = 0;
       else if (hn) kind = 1;
-      lp = cx.ot[buf][pos];
+      lp = sel(cx.ot, buf)[pos];
     }
     prm.top_pos[b * prm.P + q] = pos;
     prm.top_kind[b * prm.P + q] = kind;

@@ -5,7 +5,21 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// LDS pointers are declared in address space 3 so that every access through
+// them compiles to ds_read/ds_write (a generic pointer kept in a struct would
+// become a flat access).  Debug harnesses that run device code on the host
+// define CTCX_LDS as empty.
+#ifndef CTCX_LDS
+#define CTCX_LDS __attribute__((address_space(3)))
+#endif
+
 namespace ctcx {
+
+// CTCEXT_FLAG_PHASES counters per item: 0 row load, 1 recursion, 2 grow,
+// 3 extract, 4 commit, 5 literal frames, 6 grow events, 7 frames, 8 offer
+// scoring, 9 event loops, 10 heap pushes, 11 offer chunks, 12 accepted
+// events, 13 heap pushes (count)
+constexpr int kPhaseN = 16;
 
 // One record per (item, frame, surviving beam), written in the beam's sorted
 // position k (= its branch index next frame).  16 B so a lane stores it with
@@ -43,6 +57,7 @@ struct DecodeParams {
   int32_t* top_pos;         // [B][P]  sorted position of path p at the last frame
   int32_t* top_kind;        // [B][P]  0 blank / 1 label-ending / -1 none
   T* log_prob;              // [B][P]
+  uint64_t* prof;           // optional [B][8] phase cycle counters (diagnostics)
 };
 
 struct TraceParams {
@@ -76,7 +91,7 @@ __host__ __device__ inline int htab_size(int W) {
 
 // LDS bytes needed by the decode kernel (host + device agree on the carve).
 __host__ __device__ inline size_t decode_lds_bytes(int W, int64_t C, int tsize) {
-  const size_t ENC = 2 * (size_t)W + 2;
+  const size_t ENC = 3 * (size_t)W + 2;
   auto a16 = [](size_t v) { return (v + 15) & ~(size_t)15; };
   size_t s = 0;
   s += 2 * a16(5 * (size_t)W * tsize);          // branch probs, 2 buffers

@@ -20,16 +20,18 @@
 
 #include <stdint.h>
 
+#include "ctcx_kernels.h"
+
 namespace ctcx {
 
 template <typename T>
 struct SlotGreater {
-  const T* tot;
+  const CTCX_LDS T* tot;
   __host__ __device__ __forceinline__ bool operator()(int a, int b) const { return tot[a] > tot[b]; }
 };
 
 template <class Cmp>
-__host__ __device__ void lit_push_heap(int* e, int hole, int top, int value, const Cmp& gt) {
+__host__ __device__ void lit_push_heap(CTCX_LDS int* e, int hole, int top, int value, const Cmp& gt) {
   int parent = (hole - 1) / 2;
   while (hole > top && gt(e[parent], value)) {
     e[hole] = e[parent];
@@ -40,7 +42,7 @@ __host__ __device__ void lit_push_heap(int* e, int hole, int top, int value, con
 }
 
 template <class Cmp>
-__host__ __device__ void lit_adjust_heap(int* e, int hole, int len, int value, const Cmp& gt) {
+__host__ __device__ void lit_adjust_heap(CTCX_LDS int* e, int hole, int len, int value, const Cmp& gt) {
   const int top = hole;
   int second = hole;
   while (second < (len - 1) / 2) {
@@ -58,7 +60,7 @@ __host__ __device__ void lit_adjust_heap(int* e, int hole, int len, int value, c
 }
 
 template <class Cmp>
-__host__ __device__ void lit_make_heap(int* e, int len, const Cmp& gt) {
+__host__ __device__ void lit_make_heap(CTCX_LDS int* e, int len, const Cmp& gt) {
   if (len < 2) return;
   for (int parent = (len - 2) / 2;; --parent) {
     lit_adjust_heap(e, parent, len, e[parent], gt);
@@ -68,7 +70,7 @@ __host__ __device__ void lit_make_heap(int* e, int len, const Cmp& gt) {
 
 // std::pop_heap(e, e + len): the front moves to e[len-1].
 template <class Cmp>
-__host__ __device__ void lit_pop_heap(int* e, int len, const Cmp& gt) {
+__host__ __device__ void lit_pop_heap(CTCX_LDS int* e, int len, const Cmp& gt) {
   if (len > 1) {
     const int value = e[len - 1];
     e[len - 1] = e[0];
@@ -77,7 +79,7 @@ __host__ __device__ void lit_pop_heap(int* e, int len, const Cmp& gt) {
 }
 
 template <class Cmp>
-__host__ __device__ void lit_sort_heap(int* e, int len, const Cmp& gt) {
+__host__ __device__ void lit_sort_heap(CTCX_LDS int* e, int len, const Cmp& gt) {
   while (len > 1) {
     lit_pop_heap(e, len, gt);
     --len;
@@ -85,7 +87,7 @@ __host__ __device__ void lit_sort_heap(int* e, int len, const Cmp& gt) {
 }
 
 template <class Cmp>
-__host__ __device__ void lit_insertion_sort(int* e, int first, int last, const Cmp& gt) {
+__host__ __device__ void lit_insertion_sort(CTCX_LDS int* e, int first, int last, const Cmp& gt) {
   if (first == last) return;
   for (int i = first + 1; i != last; ++i) {
     const int v = e[i];
@@ -101,7 +103,7 @@ __host__ __device__ void lit_insertion_sort(int* e, int first, int last, const C
 }
 
 template <class Cmp>
-__host__ __device__ void lit_unguarded_insertion_sort(int* e, int first, int last, const Cmp& gt) {
+__host__ __device__ void lit_unguarded_insertion_sort(CTCX_LDS int* e, int first, int last, const Cmp& gt) {
   for (int i = first; i != last; ++i) {
     const int v = e[i];
     int k = i;
@@ -111,7 +113,7 @@ __host__ __device__ void lit_unguarded_insertion_sort(int* e, int first, int las
 }
 
 template <class Cmp>
-__host__ __device__ void lit_move_median_to_first(int* e, int result, int a, int b, int c, const Cmp& gt) {
+__host__ __device__ void lit_move_median_to_first(CTCX_LDS int* e, int result, int a, int b, int c, const Cmp& gt) {
   int pick;
   if (gt(e[a], e[b])) {
     if (gt(e[b], e[c])) pick = b;
@@ -124,7 +126,7 @@ __host__ __device__ void lit_move_median_to_first(int* e, int result, int a, int
 }
 
 template <class Cmp>
-__host__ __device__ int lit_unguarded_partition(int* e, int first, int last, int pivot, const Cmp& gt) {
+__host__ __device__ int lit_unguarded_partition(CTCX_LDS int* e, int first, int last, int pivot, const Cmp& gt) {
   while (true) {
     while (gt(e[first], e[pivot])) ++first;
     --last;
@@ -139,7 +141,7 @@ __host__ __device__ int lit_unguarded_partition(int* e, int first, int last, int
 // sub-ranges it sorts are disjoint, so the order in which they are finished
 // does not change the result.
 template <class Cmp>
-__host__ __device__ void lit_sort(int* e, int n, const Cmp& gt) {
+__host__ __device__ void lit_sort(CTCX_LDS int* e, int n, const Cmp& gt) {
   if (n <= 1) return;
   int lg = 31 - __builtin_clz((unsigned)n);
   struct Frame { int first, last, depth; };
@@ -176,7 +178,7 @@ __host__ __device__ void lit_sort(int* e, int n, const Cmp& gt) {
 enum { kTopUnordered = 0, kTopBottomKnown = 1, kTopHeap = 2 };
 
 struct LitTop {
-  int* e;      // capacity limit + 1
+  CTCX_LDS int* e;   // capacity limit + 1
   int n;       // elements_.size()
   int limit;
   int state;

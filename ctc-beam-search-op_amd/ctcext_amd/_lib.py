@@ -21,10 +21,12 @@ CTCEXT_F32 = 0
 CTCEXT_F64 = 1
 CTCEXT_FLAG_FORCE_LITERAL = 1
 CTCEXT_FLAG_PROFILE = 2
+CTCEXT_FLAG_PHASES = 4
 
 # every symbol include/ctcext.h declares
 EXPORTED_SYMBOLS = ("ctcext_create", "ctcext_destroy", "ctcext_decode", "ctcext_fetch",
-                    "ctcext_get_stats", "ctcext_last_error", "ctcext_max_beam_width")
+                    "ctcext_get_stats", "ctcext_last_error", "ctcext_max_beam_width",
+                    "ctcext_phase_counters")
 
 
 class DecodeArgs(ctypes.Structure):
@@ -96,5 +98,7 @@ def load():
     lib.ctcext_last_error.restype = ctypes.c_char_p
     lib.ctcext_max_beam_width.argtypes = [ctypes.c_int64, ctypes.c_int32]
     lib.ctcext_max_beam_width.restype = ctypes.c_int32
+    lib.ctcext_phase_counters.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
+    lib.ctcext_phase_counters.restype = ctypes.c_int
     _lib = lib
     return lib

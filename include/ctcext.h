@@ -40,7 +40,8 @@ enum { CTCEXT_F32 = 0, CTCEXT_F64 = 1 };   /* attr T: {float, double} (ops.cc:24
 
 enum {
   CTCEXT_FLAG_FORCE_LITERAL = 1,   /* testing: replay every frame through the literal TopN model */
-  CTCEXT_FLAG_PROFILE = 2          /* time the decode kernel with HIP events (ctcext_stats) */
+  CTCEXT_FLAG_PROFILE = 2,         /* time the decode kernel with HIP events (ctcext_stats) */
+  CTCEXT_FLAG_PHASES = 4           /* diagnostics: per-item s_memtime phase counters */
 };
 
 typedef struct ctcext_decoder ctcext_decoder;
@@ -106,6 +107,12 @@ int ctcext_decode(ctcext_decoder* dec, const ctcext_decode_args* args, ctcext_pa
 int ctcext_fetch(ctcext_decoder* dec, const ctcext_outputs* out);
 
 int ctcext_get_stats(ctcext_decoder* dec, ctcext_stats* stats);
+
+/* Diagnostics: copies the [batch][16] phase counters of the last decode run
+ * with CTCEXT_FLAG_PHASES (cycles: row load, recursion, grow, extract, commit,
+ * literal frames; counts: grow events, frames; cycles: offer scoring, event
+ * loops, heap pushes; counts: offer chunks, accepted events, heap pushes). */
+int ctcext_phase_counters(ctcext_decoder* dec, uint64_t* out, int64_t n);
 
 /* Message of the last failing call on this thread ("" if none). */
 const char* ctcext_last_error(void);

@@ -1,0 +1,26 @@
+"""Diagnostic: per-phase cycle split of ctcx_beam_decode (s_memtime stamps)."""
+import ctypes, os, sys
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ctc-beam-search-op_amd"))
+import numpy as np
+import torch
+import ctcext_amd
+from ctcext_amd import _lib
+B, T, W, P, C = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]) if len(sys.argv) > 5 else 29
+x = torch.as_tensor(np.random.default_rng(20251015).standard_normal((T, B, C), dtype=np.float32), device="cuda")
+sl = torch.full((B,), T, dtype=torch.int32, device="cuda")
+f = _lib.CTCEXT_FLAG_PHASES | _lib.CTCEXT_FLAG_PROFILE
+ctcext_amd.ctc_ext_beam_search_decoder(x, sl, W, P, merge_repeated=True, flags=f)
+out = ctcext_amd.ctc_ext_beam_search_decoder(x, sl, W, P, merge_repeated=True, flags=f)
+d = ctcext_amd.get_decoder(0)
+buf = np.zeros((B, 16), np.uint64)
+d.lib.ctcext_phase_counters(d.handle, ctypes.c_void_p(buf.ctypes.data), B * 16)
+m = buf.astype(np.float64).mean(0)
+fr = m[7]
+names = ["rowload", "recursion", "grow", "extract", "commit", "literal", "events", "frames",
+         "scoring", "eventloop", "heappush", "chunks", "accepted", "pushes"]
+CYC = {0, 1, 2, 3, 4, 5, 8, 9, 10}
+print("B=%d T=%d W=%d P=%d C=%d decode_ms=%.1f" % (B, T, W, P, C, d.last_stats["decode_kernel_ms"]))
+for k in range(14):
+    if k == 7:
+        continue
+    print("  %-10s %12.0f %s/frame" % (names[k], m[k] / fr, "cycles" if k in CYC else "count"))
