@@ -20,8 +20,8 @@
 namespace ctcx {
 template <typename T>
 hipError_t launch_decode(const DecodeParams<T>& p, hipStream_t s);
-hipError_t launch_row_norm_f32(const float* x, const int32_t* sl, float* norm, int64_t T, int64_t B, int64_t C,
-                               hipStream_t s);
+template <typename T>
+hipError_t launch_row_norm(const T* x, const int32_t* sl, T* norm, int64_t T_, int64_t B, int64_t C, hipStream_t s);
 hipError_t launch_traceback(const TraceParams& tp, hipStream_t s);
 hipError_t launch_scan(const int32_t* len, int64_t* off, int64_t* res, int64_t B, int P, hipStream_t s);
 hipError_t launch_pack(const PackParams& pp, hipStream_t s);
@@ -184,11 +184,7 @@ static int run_decode(ctcext_decoder* d, const ctcext_decode_args* a, const T* x
   HIP_OR_FAIL(d->h_res.ensure(8 * (size_t)(P * 4) + 16));
 
   if (prof) HIP_OR_FAIL(hipEventRecord(d->ev[0], s));
-  if (sizeof(T) == 4) {
-    HIP_OR_FAIL(ctcx::launch_row_norm_f32((const float*)x, sl, (float*)d->norm.p, T_, B, C, s));
-  } else {
-    return fail(CTCEXT_UNIMPLEMENTED, "T=double is not implemented yet on the device path");
-  }
+  HIP_OR_FAIL(ctcx::launch_row_norm<T>(x, sl, (T*)d->norm.p, T_, B, C, s));
   if (prof) HIP_OR_FAIL(hipEventRecord(d->ev[1], s));
 
   ctcx::DecodeParams<T> p{};

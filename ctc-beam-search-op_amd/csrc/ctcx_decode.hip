@@ -32,6 +32,7 @@
 #include "ctcx_kernels.h"
 #include "ctcx_topn.h"
 #include "glibc_math.h"
+#include "glibc_math_f64.h"
 
 namespace ctcx {
 
@@ -1007,19 +1008,27 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
 // ---------------------------------------------------------------------------
 // Softmax normaliser per row (decoder.h:72-80): max, sequential sum of
 // exp(x - max) in T precision, log.  Rows past an item's length are skipped.
-__global__ __launch_bounds__(256) void ctcx_row_norm_f32(const float* __restrict__ x, const int32_t* seq_len,
-                                                        float* __restrict__ norm, int64_t Tmax, int64_t B,
-                                                        int64_t C) {
+// Softmax normaliser per (t, b) row (decoder.h:72-80): sequential max, then a
+// sequential sum of exp(x_j - max) in class order, norm = max + log(sum), with
+// T's libm (float: expf/logf; double: exp/log), one thread per row.
+__host__ __device__ __forceinline__ float norm_exp(float x) { return gm::expf(x); }
+__host__ __device__ __forceinline__ double norm_exp(double x) { return gm::exp(x); }
+__host__ __device__ __forceinline__ float norm_log(float x) { return gm::logf(x); }
+__host__ __device__ __forceinline__ double norm_log(double x) { return gm::log(x); }
+
+template <typename T>
+__global__ __launch_bounds__(256) void ctcx_row_norm(const T* __restrict__ x, const int32_t* seq_len,
+                                                    T* __restrict__ norm, int64_t Tmax, int64_t B, int64_t C) {
   const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (row >= Tmax * B) return;
   const int64_t t = row / B, b = row - t * B;
   if (t >= seq_len[b]) return;
-  const float* r = x + row * C;
-  float m = r[0];
+  const T* r = x + row * C;
+  T m = r[0];
   for (int64_t j = 1; j < C; ++j) m = (r[j] > m) ? r[j] : m;
-  float s = 0.0f;
-  for (int64_t j = 0; j < C; ++j) s += gm::expf(r[j] - m);
-  norm[row] = m + gm::logf(s);
+  T s = T(0);
+  for (int64_t j = 0; j < C; ++j) s += norm_exp(r[j] - m);
+  norm[row] = m + norm_log(s);
 }
 
 // ---------------------------------------------------------------------------
@@ -1146,13 +1155,16 @@ hipError_t launch_decode(const DecodeParams<T>& p, hipStream_t s) {
 template hipError_t launch_decode<float>(const DecodeParams<float>&, hipStream_t);
 template hipError_t launch_decode<double>(const DecodeParams<double>&, hipStream_t);
 
-hipError_t launch_row_norm_f32(const float* x, const int32_t* sl, float* norm, int64_t T, int64_t B, int64_t C,
-                               hipStream_t s) {
-  const int64_t rows = T * B;
+template <typename T>
+hipError_t launch_row_norm(const T* x, const int32_t* sl, T* norm, int64_t T_, int64_t B, int64_t C, hipStream_t s) {
+  const int64_t rows = T_ * B;
   if (rows == 0) return hipSuccess;
-  hipLaunchKernelGGL(ctcx_row_norm_f32, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, x, sl, norm, T, B, C);
+  hipLaunchKernelGGL(ctcx_row_norm<T>, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, x, sl, norm, T_, B, C);
   return hipGetLastError();
 }
+template hipError_t launch_row_norm<float>(const float*, const int32_t*, float*, int64_t, int64_t, int64_t, hipStream_t);
+template hipError_t launch_row_norm<double>(const double*, const int32_t*, double*, int64_t, int64_t, int64_t,
+                                            hipStream_t);
 
 hipError_t launch_traceback(const TraceParams& tp, hipStream_t s) {
   const int64_t n = tp.B * tp.P * 2;

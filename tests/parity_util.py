@@ -33,15 +33,15 @@ def compare(out, ref, top_paths, lp_exact=True):
         np.testing.assert_allclose(lp, ref.log_probability, rtol=0, atol=1e-5)
 
 
-def random_case(rng, T_max=40, B_max=3, C_max=11, W_max=15, ties=False, neg_inf=False):
+def random_case(rng, T_max=40, B_max=3, C_max=11, W_max=15, ties=False, neg_inf=False, dtype=np.float32):
     T = int(rng.integers(1, T_max + 1))
     B = int(rng.integers(1, B_max + 1))
     C = int(rng.integers(2, C_max + 1))
     W = int(rng.integers(1, W_max + 1))
     P = int(rng.integers(1, W + 1))
-    x = rng.standard_normal((T, B, C)).astype(np.float32)
+    x = rng.standard_normal((T, B, C)).astype(dtype)
     if ties:
-        x = (np.round(x * 2) / 2).astype(np.float32)
+        x = (np.round(x * 2) / 2).astype(dtype)
     if neg_inf:
         x[rng.random(x.shape) < 0.15] = -np.inf
     sl = rng.integers(max(T // 2, 0), T + 1, size=B).astype(np.int32)

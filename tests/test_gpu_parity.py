@@ -213,3 +213,55 @@ def test_cfg2_full_length_parity():
     out, err = _gpu_or_error(x, sl, 64, 1, kw, device=True)
     assert err is None, err
     compare(out, ref, 1)
+
+
+# ---- T=double (the reference's own test runs float64, test.py:25) ----------
+
+@pytest.mark.parametrize("device", [False, True])
+def test_paper_golden_f64(device):
+    a = GOLD["attrs"]
+    logits = np.log(np.asarray(GOLD["probs"], np.float64))
+    out, err = _gpu_or_error(logits, np.asarray(GOLD["sequence_length"], np.int32), a["beam_width"],
+                             a["top_paths"], dict(merge_repeated=a["merge_repeated"],
+                                                  blank_index=a["blank_index"],
+                                                  blank_label=a["blank_label"]), device=device)
+    assert err is None, err
+    assert to_numpy(out.log_probability).dtype == np.float64
+    for p in range(a["top_paths"]):
+        np.testing.assert_array_equal(to_numpy(out.decoded_values[p]), GOLD["decoded_values"][p])
+        np.testing.assert_array_equal(to_numpy(out.alignment_values[p]), GOLD["alignment_values"][p])
+        np.testing.assert_array_equal(to_numpy(out.alignment_indices[p]), GOLD["alignment_indices"][p])
+    np.testing.assert_allclose(to_numpy(out.log_probability), GOLD["log_probability"], rtol=1e-6, atol=1e-6)
+    ref = oracle.decode(logits, GOLD["sequence_length"], a["beam_width"], a["top_paths"],
+                        a["merge_repeated"], a["blank_index"], a["blank_label"])
+    compare(out, ref, a["top_paths"])
+
+
+def test_random_small_f64():
+    _run_random(2468, 100, dtype=np.float64)
+
+
+def test_random_tie_heavy_f64():
+    _run_random(8642, 60, ties=True, dtype=np.float64)
+
+
+def test_force_literal_f64():
+    rng = np.random.default_rng(55)
+    for it in range(20):
+        x, sl, W, P, kw = random_case(rng, ties=bool(it % 2), dtype=np.float64)
+        ref, rerr = oracle_or_error(x, sl, W, P, kw)
+        out, gerr = _gpu_or_error(x, sl, W, P, kw, flags=_lib.CTCEXT_FLAG_FORCE_LITERAL)
+        assert rerr == gerr, (it, rerr, gerr)
+        if ref is not None:
+            compare(out, ref, P)
+
+
+def test_cfg3_shape_parity_f64():
+    rng = np.random.default_rng(20251017)
+    x = rng.standard_normal((300, 2, 29))
+    sl = np.array([300, 260], np.int32)
+    kw = dict(merge_repeated=True, blank_index=0, blank_label=-1)
+    ref = oracle.decode(x, sl, 128, 3, **kw)
+    out, err = _gpu_or_error(x, sl, 128, 3, kw, device=True)
+    assert err is None, err
+    compare(out, ref, 3)
