@@ -357,6 +357,42 @@ __device__ void wave_make_heap(CTCX_LDS HE<T>* he, int len) {
   }
 }
 
+// Ancestors of 1-based heap node J (J >> 1, J >> 2, ..., 1, i.e. 0-based
+// positions (J >> k) - 1): anc has a bit at each ancestor's position and req
+// the direction that ancestor's min child must take for J to be on its min
+// path (1 = right, i.e. J's bit just below the ancestor's prefix is 1).
+// Lane constants: the compiler hoists them out of every loop.
+__device__ __forceinline__ void anc_bits(unsigned J, unsigned& anc, unsigned& req) {
+  // fixed trip count, no branches: straight-line in the lane id, so hoisted
+  anc = 0;
+  req = 0;
+#pragma unroll
+  for (int k = 1; k <= 6; ++k) {   // J <= 64: at most 6 ancestors, all below position 32
+    const unsigned a = J >> k;
+    const unsigned pos = (a - 1u) & 31u;
+    const unsigned on = a != 0u ? 1u : 0u;
+    anc |= on << pos;
+    req |= (on & (J >> (k - 1))) << pos;
+  }
+}
+template <int NW>
+__device__ __forceinline__ void anc_bits_wide(unsigned J, uint64_t (&anc)[NW], uint64_t (&req)[NW]) {
+#pragma unroll
+  for (int w = 0; w < NW; ++w) { anc[w] = 0; req[w] = 0; }
+#pragma unroll
+  for (int k = 1; k <= 8; ++k) {   // J <= 256
+    const unsigned a = J >> k;
+    const unsigned pos = a - 1u;
+    const uint64_t on = a != 0u ? 1ull : 0ull;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const uint64_t here = ((pos >> 6) == (unsigned)w) ? on : 0ull;
+      anc[w] |= here << (pos & 63u);
+      req[w] |= (here & (uint64_t)(J >> (k - 1))) << (pos & 63u);
+    }
+  }
+}
+
 // __adjust_heap(0, len, v) for the whole wave.  The hole descends along the
 // smaller child (right on ties) to a leaf and v then rises while its parent is
 // strictly greater; since values along that path are non-decreasing, v stops
@@ -373,7 +409,6 @@ __device__ void wave_make_heap(CTCX_LDS HE<T>* he, int len) {
 // v, the result and all other uniform values stay in VGPRs.
 template <typename T, int RN>
 __device__ __forceinline__ HE<T> wave_adjust_heap(CTCX_LDS HE<T>* he, int len, HE<T> v, int vpos = -1) {
-  constexpr int KMAX = 6 + (RN >= 2 ? 1 : 0) + (RN >= 4 ? 1 : 0);   // depth bound of a lane node
   const int lane = threadIdx.x;
   len = uni(len);
   const int nint = len / 2;   // nodes with at least one child
@@ -402,24 +437,18 @@ __device__ __forceinline__ HE<T> wave_adjust_heap(CTCX_LDS HE<T>* he, int len, H
 #pragma unroll
   for (int r = 0; r < RN; ++r) {
     const unsigned j = (unsigned)(r * 64 + lane);
-    const unsigned J = j + 1u;
-    const int dj = 31 - __builtin_clz(J);
-    unsigned mis = 0;   // bit k-1: the depth-(dj-k) ancestor's min child is not toward j
+    unsigned mis;   // nonzero: some ancestor's min child is not the one toward j
+    if (RN == 1) {
+      unsigned anc, req;
+      anc_bits(j + 1u, anc, req);
+      mis = ((unsigned)bm[0] ^ req) & anc;   // ancestors of nodes < 64 are < 32
+    } else {
+      uint64_t anc[RN > 1 ? RN / 2 : 1], req[RN > 1 ? RN / 2 : 1];
+      anc_bits_wide<(RN > 1 ? RN / 2 : 1)>(j + 1u, anc, req);
+      mis = 0;
 #pragma unroll
-    for (int k = 1; k <= KMAX; ++k) {
-      const unsigned pos = (J >> k) - 1u;   // wraps past the root: masked by dj below
-      unsigned have;
-      if (RN == 1) {
-        have = (unsigned)bm[0] >> (pos & 31u);   // ancestors of nodes < 64 are < 32
-      } else {
-        uint64_t w = bm[0];
-#pragma unroll
-        for (int rr = 1; rr < RN / 2; ++rr) w = ((pos >> 6) == (unsigned)rr) ? bm[rr] : w;
-        have = (unsigned)(w >> (pos & 63u));
-      }
-      mis |= ((have ^ (J >> (k - 1))) & 1u) << (k - 1);
+      for (int w = 0; w < (RN > 1 ? RN / 2 : 1); ++w) mis |= ((bm[w] ^ req[w]) & anc[w]) != 0ull ? 1u : 0u;
     }
-    mis &= (1u << dj) - 1u;
     offp[r] = mis | (j >= (unsigned)nint ? 1u : 0u);
     gtv[r] = (cv[r] > v.v) ? 1u : 0u;
     const unsigned leaf = (2u * j + 1u + pk[r] >= (unsigned)nint) ? 1u : 0u;
@@ -586,6 +615,51 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     int nev = 0;
     uint64_t done = 0;
     while (true) {
+      if (st == kTopHeap) {
+        // HEAP_SORTED (the beam is full): every wanted new child is accepted
+        // and replaces the front; a re-offered evicted branch is accepted iff
+        // it beats the bottom.  Per-lane flags are kept as wave masks so one
+        // compare per event feeds both decisions.
+        uint64_t liveM = __ballot(live), cevM = __ballot(cev);
+        for (;;) {
+          const uint64_t gtM = __ballot(s > bottom);
+          const uint64_t m = liveM & ((isbm & cevM) | (~isbm & gtM)) & ~done;
+          if (m == 0) break;
+          const int k = (int)__builtin_ctzll(m);
+          done = (k == 63) ? ~0ull : ((2ull << k) - 1ull);
+          const int k_c = bcast(c, k);
+          const T k_s = bcast(s, k);
+          if (((isbm & ~gtM) >> k) & 1ull) {
+            // re-offered evicted branch rejected -> deactivated (decoder.h:200-205)
+            evr = (lane == nev) ? (k_c | kDeactRec) : evr;
+            nev += 1;
+            liveM &= ~__ballot(i == k_c);
+            continue;
+          }
+          const int fsl = front.s;
+          const bool evb = fsl < nb;
+          int slot;
+          if ((isbm >> k) & 1ull) {
+            slot = k_c;
+          } else {
+            slot = evb ? nextfree : fsl;
+            nextfree += evb ? 1 : 0;
+          }
+          myslot = (myslot == fsl) ? -1 : myslot;
+          evr = (evb && lane == nev) ? fsl : evr;
+          nev += evb ? 1 : 0;
+          myslot = (lane == k) ? slot : myslot;
+          cevM |= isbm & __ballot(evb && c == fsl);
+          HE<T> nv;
+          nv.v = k_s;
+          nv.s = slot;
+          front = wave_adjust_heap<T, RN>(he, W, nv);   // push = pop_heap(W + 1)
+          bottom = front.v;
+        }
+        live = (liveM >> lane) & 1ull;
+        cev = (cevM >> lane) & 1ull;
+        break;
+      }
       const bool want = live && (isbc ? cev : (s > (full ? bottom : NI)));
       const bool acc = !isbc || (s > NI && (!full || s > bottom));
       const uint64_t m = __ballot(want) & ~done;
@@ -595,9 +669,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       const bool k_isbc = (isbm >> k) & 1ull;
       const bool accept = (__ballot(acc) >> k) & 1ull;
       const int k_c = bcast(c, k);
-      if (pc) pc[6] += 1;
       if (accept) {
-        if (pc) pc[12] += 1;
         const T k_s = bcast(s, k);
         // the evicted bottom is the front (decoder.h:192-198)
         const int fsl = front.s;
@@ -613,11 +685,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
         HE<T> nv;
         nv.v = k_s;
         nv.s = slot;
-        if (st == kTopHeap) {
-          uint64_t th0 = pc ? __builtin_amdgcn_s_memtime() : 0;
-          front = wave_adjust_heap<T, RN>(he, W, nv);   // push = pop_heap(W + 1)
-          if (pc) { pc[10] += __builtin_amdgcn_s_memtime() - th0; pc[13] += 1; }
-        } else {
+        {
           // UNORDERED (not full) appends; BOTTOM_KNOWN only ever sees a push right
           // after its front was evicted (-inf), so the swap check never fires
           if (full && lane == 0) he[1].v = NI;
