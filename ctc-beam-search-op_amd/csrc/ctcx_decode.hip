@@ -393,6 +393,43 @@ __device__ __forceinline__ void anc_bits_wide(unsigned J, uint64_t (&anc)[NW], u
   }
 }
 
+// Per-lane constants of the sift over a heap of `len` elements (lane j owns
+// nodes j + 64 r).  Computed once per length: the push loop's length is fixed.
+template <int RN>
+struct HeapGeo {
+  int nint;                          // nodes with at least one child (uniform)
+  int dum;                           // he index of this lane's dummy store slot
+  int pair[RN];                      // he index of the child pair of node min(j, nint - 1)
+  unsigned has_r[RN];                // that node has a right child
+  unsigned off[RN];                  // node j has no children (not on any sift path)
+  unsigned leaf_l[RN], leaf_r[RN];   // its left / right child has no children
+  unsigned anc[RN], req[RN];         // RN == 1: ancestor bits / required directions
+  uint64_t anc_w[RN][RN > 1 ? RN / 2 : 1], req_w[RN][RN > 1 ? RN / 2 : 1];
+};
+
+template <int RN>
+__device__ __forceinline__ HeapGeo<RN> heap_geo(int len, int dum_base) {
+  HeapGeo<RN> g;
+  const int lane = threadIdx.x;
+  len = uni(len);
+  g.nint = len / 2;
+  g.dum = dum_base + lane;
+  const int imax = g.nint > 0 ? g.nint - 1 : 0;
+#pragma unroll
+  for (int r = 0; r < RN; ++r) {
+    const int j = r * 64 + lane;
+    const int i = min(j, imax);
+    g.pair[r] = 2 * i + 2;
+    g.has_r[r] = (2 * i + 2 < len) ? 1u : 0u;
+    g.off[r] = (j >= g.nint) ? 1u : 0u;
+    g.leaf_l[r] = (2 * j + 1 >= g.nint) ? 1u : 0u;
+    g.leaf_r[r] = (2 * j + 2 >= g.nint) ? 1u : 0u;
+    if (RN == 1) anc_bits((unsigned)j + 1u, g.anc[r], g.req[r]);
+    else anc_bits_wide<(RN > 1 ? RN / 2 : 1)>((unsigned)j + 1u, g.anc_w[r], g.req_w[r]);
+  }
+  return g;
+}
+
 // __adjust_heap(0, len, v) for the whole wave.  The hole descends along the
 // smaller child (right on ties) to a leaf and v then rises while its parent is
 // strictly greater; since values along that path are non-decreasing, v stops
@@ -402,29 +439,27 @@ __device__ __forceinline__ void anc_bits_wide(unsigned J, uint64_t (&anc)[NW], u
 // every VALU -> scalar hand-off, so the path is found lane-parallel instead of
 // by walking it: every lane loads the child pair of its node(s) (one LDS
 // batch), one ballot gives the min-child directions of all nodes, each lane
-// checks in integer arithmetic that every ancestor of its node points toward
-// it (its node is then on the path), and a second ballot + find-first-set
-// yields the stop.  All writes are one parallel store.  If vpos >= 0 v is read
-// from position vpos in the same LDS batch (pop_heap).  Returns the new root;
-// v, the result and all other uniform values stay in VGPRs.
+// checks with its precomputed ancestor masks that every ancestor of its node
+// points toward it (its node is then on the path), and a second ballot +
+// find-first-set yields the stop.  Every lane then stores unconditionally --
+// to its real target or to its dummy slot -- so no exec-mask blocks.  If
+// vpos >= 0 v is read from position vpos in the same LDS batch (pop_heap).
+// Returns the new root.
 template <typename T, int RN>
-__device__ __forceinline__ HE<T> wave_adjust_heap(CTCX_LDS HE<T>* he, int len, HE<T> v, int vpos = -1) {
+__device__ __forceinline__ HE<T> wave_adjust_heap(CTCX_LDS HE<T>* he, const HeapGeo<RN>& g, HE<T> v,
+                                                  int vpos = -1) {
   const int lane = threadIdx.x;
-  len = uni(len);
-  const int nint = len / 2;   // nodes with at least one child
-  const int imax = nint > 0 ? nint - 1 : 0;
   if (vpos >= 0) v = he_ld(he, uni(vpos) + 1);
   HE<T> L[RN], R[RN];
 #pragma unroll
-  for (int r = 0; r < RN; ++r) he_ld2(he, 2 * min(r * 64 + lane, imax) + 2, L[r], R[r]);
+  for (int r = 0; r < RN; ++r) he_ld2(he, g.pair[r], L[r], R[r]);
   T cv[RN];
   int cs[RN];
   unsigned pk[RN];
   uint64_t bm[RN];
 #pragma unroll
   for (int r = 0; r < RN; ++r) {
-    const int i = min(r * 64 + lane, imax);
-    const bool pick_r = (2 * i + 2 < len) && !(R[r].v > L[r].v);
+    const bool pick_r = g.has_r[r] && !(R[r].v > L[r].v);
     bm[r] = __ballot(pick_r);
     pk[r] = pick_r ? 1u : 0u;
     cv[r] = pick_r ? R[r].v : L[r].v;
@@ -436,40 +471,37 @@ __device__ __forceinline__ HE<T> wave_adjust_heap(CTCX_LDS HE<T>* he, int len, H
   unsigned offp[RN], gtv[RN];
 #pragma unroll
   for (int r = 0; r < RN; ++r) {
-    const unsigned j = (unsigned)(r * 64 + lane);
-    unsigned mis;   // nonzero: some ancestor's min child is not the one toward j
+    unsigned mis;   // nonzero: some ancestor's min child is not the one toward this node
     if (RN == 1) {
-      unsigned anc, req;
-      anc_bits(j + 1u, anc, req);
-      mis = ((unsigned)bm[0] ^ req) & anc;   // ancestors of nodes < 64 are < 32
+      mis = ((unsigned)bm[0] ^ g.req[r]) & g.anc[r];   // ancestors of nodes < 64 are < 32
     } else {
-      uint64_t anc[RN > 1 ? RN / 2 : 1], req[RN > 1 ? RN / 2 : 1];
-      anc_bits_wide<(RN > 1 ? RN / 2 : 1)>(j + 1u, anc, req);
       mis = 0;
 #pragma unroll
-      for (int w = 0; w < (RN > 1 ? RN / 2 : 1); ++w) mis |= ((bm[w] ^ req[w]) & anc[w]) != 0ull ? 1u : 0u;
+      for (int w = 0; w < (RN > 1 ? RN / 2 : 1); ++w)
+        mis |= ((bm[w] ^ g.req_w[r][w]) & g.anc_w[r][w]) != 0ull ? 1u : 0u;
     }
-    offp[r] = mis | (j >= (unsigned)nint ? 1u : 0u);
+    offp[r] = mis | g.off[r];
     gtv[r] = (cv[r] > v.v) ? 1u : 0u;
-    const unsigned leaf = (2u * j + 1u + pk[r] >= (unsigned)nint) ? 1u : 0u;
+    const unsigned leaf = pk[r] ? g.leaf_r[r] : g.leaf_l[r];
     cm[r] = __ballot((offp[r] | ((gtv[r] | leaf) ^ 1u)) == 0u);
   }
   int kk = -1;
 #pragma unroll
   for (int r = RN - 1; r >= 0; --r)
     if (cm[r]) kk = r * 64 + (int)__builtin_ctzll(cm[r]);
-  if (kk < 0) {
-    if (lane == 0) he_st(he, 1, v);
+  if (kk < 0) {                       // no internal nodes: v is the root
+    he_st(he, lane == 0 ? 1 : g.dum, v);
   } else {
 #pragma unroll
     for (int r = 0; r < RN; ++r) {
       const int j = r * 64 + lane;
-      if (offp[r] == 0u && (j < kk || (j == kk && gtv[r] == 0u))) he_st(he, j + 1, HE<T>{cv[r], cs[r]});
-      if (j == kk) he_st(he, (gtv[r] ? j : 2 * j + 1 + (int)pk[r]) + 1, v);
+      const bool up = offp[r] == 0u && (j < kk || (j == kk && gtv[r] == 0u));
+      he_st(he, up ? j + 1 : g.dum, HE<T>{cv[r], cs[r]});
+      he_st(he, j == kk ? (gtv[r] ? j : 2 * j + 1 + (int)pk[r]) + 1 : g.dum, v);
     }
   }
   HE<T> res;
-  const bool keep = (nint == 0) || (c0 > v.v);
+  const bool keep = (g.nint == 0) || (c0 > v.v);
   res.v = keep ? v.v : c0;
   res.s = keep ? v.s : s0;
   return res;
@@ -621,7 +653,11 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
         // it beats the bottom.  Per-lane flags are kept as wave masks so one
         // compare per event feeds both decisions.
         uint64_t liveM = __ballot(live), cevM = __ballot(cev);
+        const HeapGeo<RN> geo = heap_geo<RN>(W, W + 2);
         for (;;) {
+#ifdef CTCX_FASTLOOP_PROF
+          const uint64_t q0 = __builtin_amdgcn_s_memtime();
+#endif
           const uint64_t gtM = __ballot(s > bottom);
           const uint64_t m = liveM & ((isbm & cevM) | (~isbm & gtM)) & ~done;
           if (m == 0) break;
@@ -636,6 +672,9 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
             liveM &= ~__ballot(i == k_c);
             continue;
           }
+#ifdef CTCX_FASTLOOP_PROF
+          const uint64_t q1 = __builtin_amdgcn_s_memtime();
+#endif
           const int fsl = front.s;
           const bool evb = fsl < nb;
           int slot;
@@ -653,8 +692,15 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
           HE<T> nv;
           nv.v = k_s;
           nv.s = slot;
-          front = wave_adjust_heap<T, RN>(he, W, nv);   // push = pop_heap(W + 1)
+#ifdef CTCX_FASTLOOP_PROF
+          const uint64_t q2 = __builtin_amdgcn_s_memtime();
+#endif
+          front = wave_adjust_heap<T, RN>(he, geo, nv);   // push = pop_heap(W + 1)
           bottom = front.v;
+#ifdef CTCX_FASTLOOP_PROF
+          const uint64_t q3 = __builtin_amdgcn_s_memtime();
+          if (pc) { pc[10] += q1 - q0; pc[12] += q2 - q1; pc[13] += q3 - q2; pc[6] += 1; }
+#endif
         }
         live = (liveM >> lane) & 1ull;
         cev = (cevM >> lane) & 1ull;
@@ -692,11 +738,17 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
           if (lane == 0) he_st(he, n + 1, nv);
           ++n;
           if (n == W + 1) {
+#ifdef CTCX_FASTLOOP_PROF
+            const uint64_t q4 = __builtin_amdgcn_s_memtime();
+#endif
             wave_make_heap(he, W + 1);
             const HE<T> r0 = he_ld(he, 1);
-            front = wave_adjust_heap<T, RN>(he, W, nv, W);   // pop_heap(W + 1)
+            front = wave_adjust_heap<T, RN>(he, heap_geo<RN>(W, W + 2), nv, W);   // pop_heap(W + 1)
             if (lane == 0) he_st(he, W + 1, r0);
             st = kTopHeap;
+#ifdef CTCX_FASTLOOP_PROF
+            if (pc) pc[14] += __builtin_amdgcn_s_memtime() - q4;
+#endif
           } else if (n == W) {
             return 2;   // filled mid-frame: the lazy peek is replayed literally
           }
@@ -710,6 +762,9 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       }
     }
     // flush: resets and flags first, then the surviving accepted entries
+#ifdef CTCX_FASTLOOP_PROF
+    const uint64_t q5 = __builtin_amdgcn_s_memtime();
+#endif
     if (lane < nev) {
       const int rs = evr & ~kDeactRec;
       if (evr & kDeactRec) {
@@ -727,6 +782,9 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       cx.elab[myslot] = l;
       if (isbc) __hip_atomic_fetch_and(&cx.bst[c], ~S_EVICT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+#ifdef CTCX_FASTLOOP_PROF
+    if (pc) pc[15] += __builtin_amdgcn_s_memtime() - q5;
+#endif
     if (pc) pc[9] += __builtin_amdgcn_s_memtime() - tc1;
   }
 
@@ -752,7 +810,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     // pop_heap(len): e[len-1] <- e[0], then sift the old e[len-1] from the root
     for (int len = W; len > 1; --len) {
       const HE<T> old_front = front;
-      front = wave_adjust_heap<T, RN>(he, len - 1, front, len - 1);
+      front = wave_adjust_heap<T, RN>(he, heap_geo<RN>(len - 1, W + 2), front, len - 1);
       if (lane == 0) he_st(he, len, old_front);
     }
     nout = W;

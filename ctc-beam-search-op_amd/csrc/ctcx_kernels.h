@@ -106,7 +106,7 @@ __host__ __device__ inline size_t decode_lds_bytes(int W, int64_t C, int tsize) 
   s += 64;                                      // scalars
   s += 2 * 4 * (size_t)W * 8;                   // prefix hashes (own + parent), 2 buffers
   s += a16(4 * (size_t)htab_size(W));           // per-frame new-leaf hash table
-  s += ((size_t)W + 2) * (tsize == 8 ? 16 : 8); // TopN elements (value, slot)
+  s += ((size_t)W + 2 + 64) * (tsize == 8 ? 16 : 8); // TopN elements (value, slot) + per-lane dummy slots
   return s;
 }
 

@@ -10,7 +10,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libctcext.so")
+LIB_PATH = os.environ.get("CTCEXT_LIB_PATH") or os.path.join(_HERE, "lib", "libctcext.so")   # override: diagnostics builds
 
 CTCEXT_OK = 0
 CTCEXT_INVALID_ARGUMENT = 3

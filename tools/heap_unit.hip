@@ -43,7 +43,7 @@ __global__ void heap_kernel(const float* vals, const float* reps, int len, int n
     return;
   }
   const HE<float> r0 = he_ld(he, 1);
-  HE<float> front = wave_adjust_heap<float, RN>(he, len, r0, len);
+  HE<float> front = wave_adjust_heap<float, RN>(he, heap_geo<RN>(len, len + 3), r0, len);
   if (lane == 0) he_st(he, len + 1, r0);
   if (stage == 1) {
     for (int i = lane; i < len; i += 64) out_s[i] = he[i + 1].s;
@@ -53,7 +53,7 @@ __global__ void heap_kernel(const float* vals, const float* reps, int len, int n
     HE<float> nv;
     nv.v = reps[r];
     nv.s = 1000 + r;
-    front = wave_adjust_heap<float, RN>(he, len, nv);
+    front = wave_adjust_heap<float, RN>(he, heap_geo<RN>(len, len + 3), nv);
   }
   if (stage == 2) {
     for (int i = lane; i < len; i += 64) out_s[i] = he[i + 1].s;
@@ -63,7 +63,7 @@ __global__ void heap_kernel(const float* vals, const float* reps, int len, int n
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
   for (int l = len; l > 1; --l) {
     const HE<float> old_front = front;
-    front = wave_adjust_heap<float, RN>(he, l - 1, front, l - 1);
+    front = wave_adjust_heap<float, RN>(he, heap_geo<RN>(l - 1, len + 3), front, l - 1);
     if (lane == 0) he_st(he, l, old_front);
   }
   const uint64_t t1 = __builtin_amdgcn_s_memtime();
@@ -81,19 +81,19 @@ __global__ void heap_time(const float* reps, int nrep, float* out) {
   __syncthreads();
   wave_make_heap(he, len + 1);
   const HE<float> r0 = he_ld(he, 1);
-  HE<float> front = wave_adjust_heap<float, 1>(he, len, r0, len);
+  HE<float> front = wave_adjust_heap<float, 1>(he, heap_geo<1>(len, len + 3), r0, len);
   if (lane == 0) he_st(he, len + 1, r0);
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
   for (int r = 0; r < nrep; ++r) {
     HE<float> nv;
     nv.v = reps[r] + 3.0f;
     nv.s = 1000 + r;
-    if (nv.v > front.v) front = wave_adjust_heap<float, 1>(he, len, nv);
+    if (nv.v > front.v) front = wave_adjust_heap<float, 1>(he, heap_geo<1>(len, len + 3), nv);
   }
   const uint64_t t1 = __builtin_amdgcn_s_memtime();
   for (int l = len; l > 1; --l) {
     const HE<float> old_front = front;
-    front = wave_adjust_heap<float, 1>(he, l - 1, front, l - 1);
+    front = wave_adjust_heap<float, 1>(he, heap_geo<1>(l - 1, len + 3), front, l - 1);
     if (lane == 0) he_st(he, l, old_front);
   }
   const uint64_t t2 = __builtin_amdgcn_s_memtime();
@@ -111,7 +111,7 @@ int main() {
     (void)hipMalloc(&dr, 4 * reps.size());
     (void)hipMalloc(&o, 16);
     (void)hipMemcpy(dr, reps.data(), 4 * reps.size(), hipMemcpyHostToDevice);
-    hipLaunchKernelGGL(heap_time, dim3(1), dim3(64), 8 * 136, 0, dr, nrep, o);
+    hipLaunchKernelGGL(heap_time, dim3(1), dim3(64), 8 * (136 + 64), 0, dr, nrep, o);
     (void)hipMemcpy(ho, o, 12, hipMemcpyDeviceToHost);
     printf("RN=1 W=128: %.0f cycles per push slot, %.0f cycles per sort pop\n", ho[0], ho[1]);
     (void)hipFree(dr); (void)hipFree(o);
@@ -147,11 +147,11 @@ int main() {
     (void)hipMemcpy(dv, vals.data(), 4 * (len + 1), hipMemcpyHostToDevice);
     (void)hipMemcpy(dr, reps.data(), 4 * (nrep + 1), hipMemcpyHostToDevice);
     if (len <= 128)
-      hipLaunchKernelGGL(heap_kernel<1>, dim3(1), dim3(64), 8 * (len + 4), 0, dv, dr, len, nrep, os, ov, stage);
+      hipLaunchKernelGGL(heap_kernel<1>, dim3(1), dim3(64), 8 * (len + 4 + 64), 0, dv, dr, len, nrep, os, ov, stage);
     else if (len <= 256)
-      hipLaunchKernelGGL(heap_kernel<2>, dim3(1), dim3(64), 8 * (len + 4), 0, dv, dr, len, nrep, os, ov, stage);
+      hipLaunchKernelGGL(heap_kernel<2>, dim3(1), dim3(64), 8 * (len + 4 + 64), 0, dv, dr, len, nrep, os, ov, stage);
     else
-      hipLaunchKernelGGL(heap_kernel<4>, dim3(1), dim3(64), 8 * (len + 4), 0, dv, dr, len, nrep, os, ov, stage);
+      hipLaunchKernelGGL(heap_kernel<4>, dim3(1), dim3(64), 8 * (len + 4 + 64), 0, dv, dr, len, nrep, os, ov, stage);
     std::vector<int> gs(nout);
     (void)hipMemcpy(gs.data(), os, 4 * nout, hipMemcpyDeviceToHost);
     if (stage == 3 && it < 12) {

@@ -90,7 +90,7 @@ __device__ __forceinline__ HE<float> adj(CTCX_LDS HE<float>* he, int len, int vp
 
 template <int MODE>
 __device__ __forceinline__ HE<float> adj_or_real(CTCX_LDS HE<float>* he, int len, int vpos) {
-  if (MODE == 6) return wave_adjust_heap<float, 1>(he, len, HE<float>{0.f, 0}, vpos);
+  if (MODE == 6) return wave_adjust_heap<float, 1>(he, heap_geo<1>(len, 131), HE<float>{0.f, 0}, vpos);
   return adj<MODE>(he, len, vpos);
 }
 
@@ -124,13 +124,13 @@ int main() {
   (void)hipMemset(o, 0, 64);
   (void)hipMemcpy(dv, v.data(), 4 * 128, hipMemcpyHostToDevice);
   for (int rep = 0; rep < 2; ++rep) {
-    hipLaunchKernelGGL(pop_time<0>, dim3(1), dim3(64), 8 * 136, 0, dv, o);
-    hipLaunchKernelGGL(pop_time<1>, dim3(1), dim3(64), 8 * 136, 0, dv, o);
-    hipLaunchKernelGGL(pop_time<2>, dim3(1), dim3(64), 8 * 136, 0, dv, o);
-    hipLaunchKernelGGL(pop_time<3>, dim3(1), dim3(64), 8 * 136, 0, dv, o);
-    hipLaunchKernelGGL(pop_time<4>, dim3(1), dim3(64), 8 * 136, 0, dv, o);
-    hipLaunchKernelGGL(pop_time<5>, dim3(1), dim3(64), 8 * 136, 0, dv, o);
-    hipLaunchKernelGGL(pop_time<6>, dim3(1), dim3(64), 8 * 136, 0, dv, o);
+    hipLaunchKernelGGL(pop_time<0>, dim3(1), dim3(64), 8 * (136 + 64), 0, dv, o);
+    hipLaunchKernelGGL(pop_time<1>, dim3(1), dim3(64), 8 * (136 + 64), 0, dv, o);
+    hipLaunchKernelGGL(pop_time<2>, dim3(1), dim3(64), 8 * (136 + 64), 0, dv, o);
+    hipLaunchKernelGGL(pop_time<3>, dim3(1), dim3(64), 8 * (136 + 64), 0, dv, o);
+    hipLaunchKernelGGL(pop_time<4>, dim3(1), dim3(64), 8 * (136 + 64), 0, dv, o);
+    hipLaunchKernelGGL(pop_time<5>, dim3(1), dim3(64), 8 * (136 + 64), 0, dv, o);
+    hipLaunchKernelGGL(pop_time<6>, dim3(1), dim3(64), 8 * (136 + 64), 0, dv, o);
   }
   (void)hipMemcpy(h, o, 64, hipMemcpyDeviceToHost);
   const char* nm[] = {"decode kernel's pop", "no chase", "chase, no stores", "unrolled branch-free chase",
