@@ -662,10 +662,10 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
           const uint64_t m = liveM & ((isbm & cevM) | (~isbm & gtM)) & ~done;
           if (m == 0) break;
           const int k = (int)__builtin_ctzll(m);
-          done = (k == 63) ? ~0ull : ((2ull << k) - 1ull);
-          const int k_c = bcast(c, k);
+          done = m ^ (m - 1ull);   // lanes <= k (k is m's lowest set bit; done's lanes are below it)
           const T k_s = bcast(s, k);
           if (((isbm & ~gtM) >> k) & 1ull) {
+            const int k_c = bcast(c, k);
             // re-offered evicted branch rejected -> deactivated (decoder.h:200-205)
             evr = (lane == nev) ? (k_c | kDeactRec) : evr;
             nev += 1;
@@ -679,7 +679,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
           const bool evb = fsl < nb;
           int slot;
           if ((isbm >> k) & 1ull) {
-            slot = k_c;
+            slot = bcast(c, k);
           } else {
             slot = evb ? nextfree : fsl;
             nextfree += evb ? 1 : 0;
