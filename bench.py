@@ -97,6 +97,7 @@ def main():
     ap.add_argument("--cpu-tcap", type=int, default=1500)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--seq-len", type=int, default=0, help="diagnostics: override T (not a bench line)")
     args = ap.parse_args()
 
     import torch
@@ -115,6 +116,8 @@ def main():
     torch.cuda.set_device(dev)
 
     cfg = CONFIGS[args.config]
+    if args.seq_len:
+        cfg = (cfg[0], args.seq_len) + cfg[2:]
     B, T, C, W, P, merge, blank = cfg
     x_np, sl_np = make_inputs(cfg, rank)
     x = torch.as_tensor(x_np, device=dev)

@@ -103,7 +103,7 @@ struct ctcext_decoder {
   ctcext_stats stats{};
 };
 
-static size_t lds_limit() { return 160 * 1024; }
+static size_t lds_limit() { return ctcx::kLdsBytes; }
 
 extern "C" int32_t ctcext_max_beam_width(int64_t num_classes, int32_t dtype) {
   const int ts = dtype == CTCEXT_F64 ? 8 : 4;

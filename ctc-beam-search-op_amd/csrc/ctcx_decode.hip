@@ -91,6 +91,16 @@ __device__ __forceinline__ T wave_min(T v) {
   return v;
 }
 
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const T w = __shfl_xor(v, o);
+    v = (w > v) ? w : v;
+  }
+  return v;
+}
+
 // "first-pushed maximum" of a std::priority_queue with a strict '<' comparer
 // (ctc_beam_entry.h:65-73): only a strictly greater push replaces the top.
 template <typename T>
@@ -165,8 +175,9 @@ struct Ctx {
   // parent's, [buf][i]; htab maps the hash of a frame's new leaves to position
   CTCX_LDS uint64_t* ha[2]; CTCX_LDS uint64_t* hb[2]; CTCX_LDS uint64_t* pha[2]; CTCX_LDS uint64_t* phb[2];
   CTCX_LDS int* htab;
+  CTCX_LDS uint64_t* bloom;   // per branch: label bits (l & 63) of children evicted this frame
   CTCX_LDS HE<T>* he;  // TopN elements_, position p at he[p + 1]
-  int W, C, blank, enc, hts;
+  int W, C, blank, enc, hts, wcap;
 };
 
 // Frame-parity buffer select without indexing the pointer pair, so Ctx stays
@@ -192,25 +203,30 @@ __host__ __device__ __forceinline__ void hmix(uint64_t a, uint64_t b, int l, uin
 }
 constexpr uint64_t kRootHa = 0x243F6A8885A308D3ull, kRootHb = 0x13198A2E03707344ull;
 
+// LDS layout for a beam of up to Wcap (the kernel's compile-time capacity, or
+// the runtime W for the WC = 0 instantiations).  Every array sits at an offset
+// that depends on Wcap only -- the C-sized logit row comes last -- so with a
+// compile-time Wcap all of them are instruction immediates instead of ~45
+// pointer SGPRs.  decode_lds_bytes (ctcx_kernels.h) mirrors this sum.
 template <typename T>
-__host__ __device__ void carve(Ctx<T>& cx, CTCX_LDS char* base, int W, int C) {
-  const size_t ENC = 3 * (size_t)W + 2;
+__host__ __device__ void carve(Ctx<T>& cx, CTCX_LDS char* base, int Wcap, int W, int C) {
+  const size_t ENC = 3 * (size_t)Wcap + 2;
   auto a16 = [](size_t v) { return (v + 15) & ~(size_t)15; };
   CTCX_LDS char* p = base;
   for (int b = 0; b < 2; ++b) {
     CTCX_LDS T* q = (CTCX_LDS T*)p;
-    cx.ot[b] = q; cx.ob[b] = q + W; cx.ol[b] = q + 2 * W; cx.cb[b] = q + 3 * W; cx.cn[b] = q + 4 * W;
-    p += a16(5 * (size_t)W * sizeof(T));
+    cx.ot[b] = q; cx.ob[b] = q + Wcap; cx.ol[b] = q + 2 * Wcap; cx.cb[b] = q + 3 * Wcap; cx.cn[b] = q + 4 * Wcap;
+    p += a16(5 * (size_t)Wcap * sizeof(T));
   }
   for (int b = 0; b < 2; ++b) {
     CTCX_LDS int* q = (CTCX_LDS int*)p;
-    cx.lab[b] = q; cx.par[b] = q + W; cx.flg[b] = q + 2 * W;
-    p += a16(3 * (size_t)W * 4);
+    cx.lab[b] = q; cx.par[b] = q + Wcap; cx.flg[b] = q + 2 * Wcap;
+    p += a16(3 * (size_t)Wcap * 4);
   }
   {
     CTCX_LDS int* q = (CTCX_LDS int*)p;
-    cx.head = q; cx.sib = q + W; cx.bst = q + 2 * W; cx.newpos = q + 3 * W;
-    p += a16(4 * (size_t)W * 4);
+    cx.head = q; cx.sib = q + Wcap; cx.bst = q + 2 * Wcap; cx.newpos = q + 3 * Wcap;
+    p += a16(4 * (size_t)Wcap * 4);
   }
   {
     CTCX_LDS T* q = (CTCX_LDS T*)p;
@@ -223,21 +239,25 @@ __host__ __device__ void carve(Ctx<T>& cx, CTCX_LDS char* base, int W, int C) {
     cx.elab = (CTCX_LDS int*)(q + 3 * ENC); cx.eflg = (CTCX_LDS int*)(q + 4 * ENC);
     p += a16(5 * ENC * 4);
   }
-  cx.heap = (CTCX_LDS int*)p; p += a16(((size_t)W + 1) * 4);
-  cx.tops = (CTCX_LDS int*)p; p += a16(((size_t)W + 1) * 4);
+  cx.heap = (CTCX_LDS int*)p; p += a16(((size_t)Wcap + 1) * 4);
+  cx.tops = (CTCX_LDS int*)p; p += a16(((size_t)Wcap + 1) * 4);
   cx.freel = (CTCX_LDS int*)p; p += a16(ENC * 4);
-  cx.sorted = (CTCX_LDS int*)p; p += a16((size_t)W * 4);
-  cx.row = (CTCX_LDS T*)p; p += a16((size_t)C * sizeof(T));
+  cx.sorted = (CTCX_LDS int*)p; p += a16((size_t)Wcap * 4);
   cx.misc = (CTCX_LDS int*)p; p += 64;
   for (int b = 0; b < 2; ++b) {
     CTCX_LDS uint64_t* q = (CTCX_LDS uint64_t*)p;
-    cx.ha[b] = q; cx.hb[b] = q + W; cx.pha[b] = q + 2 * W; cx.phb[b] = q + 3 * W;
-    p += 4 * (size_t)W * 8;
+    cx.ha[b] = q; cx.hb[b] = q + Wcap; cx.pha[b] = q + 2 * Wcap; cx.phb[b] = q + 3 * Wcap;
+    p += 4 * (size_t)Wcap * 8;
   }
-  cx.hts = htab_size(W);
+  cx.hts = htab_size(Wcap);
   cx.htab = (CTCX_LDS int*)p;
   p += a16(4 * (size_t)cx.hts);
+  cx.bloom = (CTCX_LDS uint64_t*)p;
+  p += a16(8 * (size_t)Wcap);
   cx.he = (CTCX_LDS HE<T>*)p;
+  p += ((size_t)Wcap + 2 + 64) * sizeof(HE<T>);
+  cx.row = (CTCX_LDS T*)p;
+  cx.wcap = Wcap;
   cx.W = W; cx.C = C; cx.enc = (int)ENC;
 }
 
@@ -558,17 +578,23 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
   CTCX_LDS HE<T>* he = cx.he;
 
   bool bad = !(norm > NI && norm < pinf<T>());
+  T xmax = NI;
   for (int j = lane; j < C; j += 64) {
     const T xv = cx.row[j];
     bad |= (xv != xv) || (xv == pinf<T>());
+    xmax = xv > xmax ? xv : xmax;
   }
   if (__ballot(bad)) return 1;
+  // max_l (x_l - norm): float rounding is monotone, so pmax + base bounds
+  // every offer's score p + base computed the reference's way
+  const T pmax = wave_max(xmax) - norm;
 
   // roll (decoder.h:87-92) + recursion (decoder.h:95-143), lanes over branches
   for (int i = lane; i < nb; i += 64) {
     cx.et[i] = sel(cx.ot, buf)[i]; cx.eb[i] = sel(cx.ob, buf)[i]; cx.el[i] = sel(cx.ol, buf)[i];
     cx.eflg[i] = 0;
     cx.bst[i] = 0;
+    cx.bloom[i] = 0;
   }
   __syncthreads();
   for (int i = lane; i < nb; i += 64) recurse_branch(cx, buf, i, norm, false);
@@ -607,16 +633,47 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
   // entries and the S_EVICT / S_DEACT flags are kept in registers (myslot, the
   // record list evr/nev) and flushed by all lanes at the chunk's end: nothing
   // reads them before then, and an event then costs no divergent stores.
+  // Branch turns (decoder.h:151-159): once the beam is full, branch b is
+  // skipped iff b.old.total <= bottom at the moment its turn starts; branches
+  // come in descending total and bottom only rises, so the first skipped
+  // branch ends the grow.  A chunk can hold the starts of several branches:
+  // each lane carries the bottom at its branch's start (bat); a skipped turn
+  // can only show through a re-offer (a skipped branch's new children score
+  // <= its total <= bottom), so only re-offers consult it, and the turn that
+  // continues into the next chunk is checked at the chunk's end.
+  // Skipping (ours, exact): with the beam full, an offer whose child is new and
+  // whose score is <= bottom is rejected without effect, and an offer whose
+  // child is an active branch is skipped by the reference too; only a re-offer
+  // of an evicted branch-child has an effect (deactivation).  bloom flags the
+  // labels that may be such re-offers, so the rest of a branch with
+  // pmax + ot <= bottom and no flagged label, or a chunk without any score >
+  // bottom or flagged lane, is skipped whole (what matters at large C).
   const int Cm1 = C - 1;
-  const int64_t total = (int64_t)nb * Cm1;
-  for (int64_t f0 = 0; f0 < total; f0 += 64) {
-    const int i0 = (int)(f0 / Cm1);
-    if (full && uni((int)!(sel(cx.ot, buf)[i0] > bottom))) break;   // every later branch is skipped
+  const float rcp = 1.0f / (float)Cm1;
+  int i0 = 0, li0 = 0;   // the chunk's first offer: branch i0, label index li0
+  bool stop = false;
+  while (i0 < nb && !stop) {
+    if (full && (li0 == 0 || Cm1 >= 64)) {
+      const T ot0 = sel(cx.ot, buf)[i0];
+      if (li0 == 0 && uni((int)!(ot0 > bottom))) break;   // branch i0's turn: skipped, and all later
+      // (small C: a branch spans few chunks, and the chunk test below suffices)
+      if (Cm1 >= 64 && uni((int)(!(pmax + ot0 > bottom) && cx.bloom[i0] == 0ull))) {
+        ++i0;
+        li0 = 0;
+        continue;
+      }
+    }
     const uint64_t tc0 = pc ? __builtin_amdgcn_s_memtime() : 0;
-    const int64_t f = f0 + lane;
-    const bool valid = f < total;
-    const int i = valid ? (int)(f / Cm1) : i0;
-    const int li = valid ? (int)(f - (int64_t)i * Cm1) : 0;
+    // lane -> (branch, label index): x / Cm1 for x < 64 + Cm1, by float reciprocal
+    const int x = li0 + lane;
+    int q = (int)((float)x * rcp);
+    q -= (q * Cm1 > x) ? 1 : 0;
+    q += ((q + 1) * Cm1 <= x) ? 1 : 0;
+    const int iv = i0 + q;
+    const bool valid = iv < nb;
+    const int i = valid ? iv : i0;
+    const int li = valid ? x - q * Cm1 : 0;
+    for (li0 += 64; li0 >= Cm1; li0 -= Cm1) ++i0;
     const int l = li + (li >= blank ? 1 : 0);
     const int bl = sel(cx.lab, buf)[i];
     const int bflg = sel(cx.flg, buf)[i];
@@ -625,6 +682,16 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     const T xl = cx.row[l];
     const T p = xl - norm;
     const T s = p + ((l == bl) ? sel(cx.ob, buf)[i] : bt);
+    // the lane where this lane's branch turn starts in the chunk (< 0: in an
+    // earlier chunk, found open there), and the bottom at that moment (bat:
+    // refreshed after every event for turns that start later in the chunk)
+    const int sl = lane - li;
+    T bat = sl > 0 ? bottom : NI;
+    const uint64_t startsM = __ballot(valid && li == 0 && lane != 0);   // branch turns starting mid-chunk
+    if (full && !__ballot(live && (s > bottom || ((cx.bloom[i] >> (l & 63)) & 1ull)))) {
+      if (startsM & ~__ballot(bt > bottom)) break;   // no event here: every start sees this bottom
+      continue;
+    }
     int c = -1;
     if (live) {
       for (int k = cx.head[i]; k >= 0; k = cx.sib[k])
@@ -653,7 +720,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
         // it beats the bottom.  Per-lane flags are kept as wave masks so one
         // compare per event feeds both decisions.
         uint64_t liveM = __ballot(live), cevM = __ballot(cev);
-        const HeapGeo<RN> geo = heap_geo<RN>(W, W + 2);
+        const HeapGeo<RN> geo = heap_geo<RN>(W, cx.wcap + 2);
         for (;;) {
 #ifdef CTCX_FASTLOOP_PROF
           const uint64_t q0 = __builtin_amdgcn_s_memtime();
@@ -662,6 +729,17 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
           const uint64_t m = liveM & ((isbm & cevM) | (~isbm & gtM)) & ~done;
           if (m == 0) break;
           const int k = (int)__builtin_ctzll(m);
+          if ((isbm >> k) & 1ull) {
+            // only a re-offer can make a closed turn visible (a closed branch's new
+            // children score <= its total <= bottom): was k's turn skipped?
+            const uint64_t closedM = __ballot(!(bt > bat));
+            if ((closedM >> k) & 1ull) {
+              const int k_sl = bcast(sl, k);
+              liveM &= (1ull << k_sl) - 1ull;   // that branch and every later one
+              stop = true;
+              continue;
+            }
+          }
           done = m ^ (m - 1ull);   // lanes <= k (k is m's lowest set bit; done's lanes are below it)
           const T k_s = bcast(s, k);
           if (((isbm & ~gtM) >> k) & 1ull) {
@@ -697,6 +775,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
 #endif
           front = wave_adjust_heap<T, RN>(he, geo, nv);   // push = pop_heap(W + 1)
           bottom = front.v;
+          bat = (sl > k) ? bottom : bat;
 #ifdef CTCX_FASTLOOP_PROF
           const uint64_t q3 = __builtin_amdgcn_s_memtime();
           if (pc) { pc[10] += q1 - q0; pc[12] += q2 - q1; pc[13] += q3 - q2; pc[6] += 1; }
@@ -711,6 +790,11 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       const uint64_t m = __ballot(want) & ~done;
       if (m == 0) break;
       const int k = __ffsll((unsigned long long)m) - 1;
+      if (full && ((isbm >> k) & 1ull) && ((__ballot(!(bt > bat)) >> k) & 1ull)) {
+        live = live && lane < bcast(sl, k);   // k's turn was skipped, and every later one
+        stop = true;
+        continue;
+      }
       done = (k == 63) ? ~0ull : ((2ull << k) - 1ull);
       const bool k_isbc = (isbm >> k) & 1ull;
       const bool accept = (__ballot(acc) >> k) & 1ull;
@@ -743,7 +827,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
 #endif
             wave_make_heap(he, W + 1);
             const HE<T> r0 = he_ld(he, 1);
-            front = wave_adjust_heap<T, RN>(he, heap_geo<RN>(W, W + 2), nv, W);   // pop_heap(W + 1)
+            front = wave_adjust_heap<T, RN>(he, heap_geo<RN>(W, cx.wcap + 2), nv, W);   // pop_heap(W + 1)
             if (lane == 0) he_st(he, W + 1, r0);
             st = kTopHeap;
 #ifdef CTCX_FASTLOOP_PROF
@@ -753,7 +837,10 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
             return 2;   // filled mid-frame: the lazy peek is replayed literally
           }
         }
-        if (full) bottom = front.v;
+        if (full) {
+          bottom = front.v;
+          bat = (sl > k) ? bottom : bat;
+        }
       } else {
         // re-offered evicted branch rejected -> deactivated (decoder.h:200-205)
         evr = (lane == nev) ? (k_c | kDeactRec) : evr;
@@ -761,6 +848,8 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
         live = live && (i != k_c);
       }
     }
+    // the turn continuing into the next chunk: skipped -> so is every later one
+    if (full && (__ballot(valid && !(bt > bat)) >> 63) & 1ull) stop = true;
     // flush: resets and flags first, then the surviving accepted entries
 #ifdef CTCX_FASTLOOP_PROF
     const uint64_t q5 = __builtin_amdgcn_s_memtime();
@@ -772,6 +861,10 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       } else {
         cx.et[rs] = NI; cx.eb[rs] = NI; cx.el[rs] = NI; cx.eflg[rs] = 0;
         __hip_atomic_fetch_or(&cx.bst[rs], S_EVICT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const int par = sel(cx.par, buf)[rs];
+        if (par >= 0)
+          __hip_atomic_fetch_or(&cx.bloom[par], 1ull << (sel(cx.lab, buf)[rs] & 63), __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
     if (myslot >= 0) {
@@ -810,7 +903,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     // pop_heap(len): e[len-1] <- e[0], then sift the old e[len-1] from the root
     for (int len = W; len > 1; --len) {
       const HE<T> old_front = front;
-      front = wave_adjust_heap<T, RN>(he, heap_geo<RN>(len - 1, W + 2), front, len - 1);
+      front = wave_adjust_heap<T, RN>(he, heap_geo<RN>(len - 1, cx.wcap + 2), front, len - 1);
       if (lane == 0) he_st(he, len, old_front);
     }
     nout = W;
@@ -941,11 +1034,11 @@ __host__ __device__ __attribute__((noinline)) int literal_step(Ctx<T> cx, int bu
 }
 
 // ---------------------------------------------------------------------------
-template <typename T, int RN>
+template <typename T, int RN, int WC>
 __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   Ctx<T> cx;
-  carve(cx, (CTCX_LDS char*)lds, prm.W, (int)prm.C);
+  carve(cx, (CTCX_LDS char*)lds, WC > 0 ? WC : prm.W, prm.W, (int)prm.C);
   cx.blank = prm.blank;
   const int lane = threadIdx.x;
   const int64_t b = blockIdx.x;
@@ -1257,25 +1350,27 @@ __global__ __launch_bounds__(64) void ctcx_pack(PackParams pp) {
 // Launchers (called by the C-ABI layer).
 namespace ctcx {
 
-template <typename T, int RN>
-static hipError_t launch_decode_r(const DecodeParams<T>& p, size_t lds, hipStream_t s) {
+template <typename T, int RN, int WC>
+static hipError_t launch_decode_r(const DecodeParams<T>& p, hipStream_t s) {
+  const size_t lds = decode_lds_bytes(WC > 0 ? WC : p.W, p.C, (int)sizeof(T));
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)ctcx_beam_decode<T, RN>,
+    hipError_t e = hipFuncSetAttribute((const void*)ctcx_beam_decode<T, RN, WC>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((ctcx_beam_decode<T, RN>), dim3((unsigned)p.B), dim3(64), lds, s, p);
+  hipLaunchKernelGGL((ctcx_beam_decode<T, RN, WC>), dim3((unsigned)p.B), dim3(64), lds, s, p);
   return hipGetLastError();
 }
 
 template <typename T>
 hipError_t launch_decode(const DecodeParams<T>& p, hipStream_t s) {
-  const size_t lds = decode_lds_bytes(p.W, p.C, (int)sizeof(T));
   if (p.B == 0) return hipSuccess;
-  // RN registers per lane hold the min-child of the (W + 1) / 2 internal heap nodes
-  if (p.W <= 128) return launch_decode_r<T, 1>(p, lds, s);
-  if (p.W <= 256) return launch_decode_r<T, 2>(p, lds, s);
-  return launch_decode_r<T, 4>(p, lds, s);
+  // RN registers per lane hold the min-child of the (W + 1) / 2 internal heap
+  // nodes; the compile-time layouts (WC) are used whenever they fit the LDS
+  auto fits = [&](int wc) { return decode_lds_bytes(wc, p.C, (int)sizeof(T)) <= kLdsBytes; };
+  if (p.W <= 128) return fits(128) ? launch_decode_r<T, 1, 128>(p, s) : launch_decode_r<T, 1, 0>(p, s);
+  if (p.W <= 256) return fits(256) ? launch_decode_r<T, 2, 256>(p, s) : launch_decode_r<T, 2, 0>(p, s);
+  return launch_decode_r<T, 4, 0>(p, s);
 }
 
 template hipError_t launch_decode<float>(const DecodeParams<float>&, hipStream_t);

@@ -90,23 +90,28 @@ __host__ __device__ inline int htab_size(int W) {
 }
 
 // LDS bytes needed by the decode kernel (host + device agree on the carve).
+constexpr size_t kLdsBytes = 160 * 1024;   // LDS per CU on gfx950 (one workgroup per item)
+
+// Bytes of the decode kernel's LDS layout for a beam capacity W (carve() in
+// ctcx_decode.hip, same order and alignment).
 __host__ __device__ inline size_t decode_lds_bytes(int W, int64_t C, int tsize) {
   const size_t ENC = 3 * (size_t)W + 2;
   auto a16 = [](size_t v) { return (v + 15) & ~(size_t)15; };
   size_t s = 0;
   s += 2 * a16(5 * (size_t)W * tsize);          // branch probs, 2 buffers
   s += 2 * a16(3 * (size_t)W * 4);              // branch label/parent/flags, 2 buffers
-  s += a16(4 * (size_t)W * 4);                  // head, sib, bstate, newpos
+  s += a16(4 * (size_t)W * 4);                  // child lists, state, new positions
   s += a16(5 * ENC * tsize);                    // entry probs
   s += a16(5 * ENC * 4);                        // entry bps/kind/label/flags
   s += a16(((size_t)W + 1) * 4) * 2;            // heap, top-paths scratch
   s += a16(ENC * 4);                            // free list / slot map
   s += a16((size_t)W * 4);                      // sorted
-  s += a16((size_t)C * tsize);                  // logit row
   s += 64;                                      // scalars
-  s += 2 * 4 * (size_t)W * 8;                   // prefix hashes (own + parent), 2 buffers
+  s += 2 * 4 * (size_t)W * 8;                   // prefix hashes, 2 buffers
   s += a16(4 * (size_t)htab_size(W));           // per-frame new-leaf hash table
+  s += a16(8 * (size_t)W);                      // per-branch evicted-child label bloom
   s += ((size_t)W + 2 + 64) * (tsize == 8 ? 16 : 8); // TopN elements (value, slot) + per-lane dummy slots
+  s += a16((size_t)C * tsize);                  // logit row
   return s;
 }
 

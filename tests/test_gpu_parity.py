@@ -265,3 +265,10 @@ def test_cfg3_shape_parity_f64():
     out, err = _gpu_or_error(x, sl, 128, 3, kw, device=True)
     assert err is None, err
     compare(out, ref, 3)
+
+
+def test_random_reoffer_heavy():
+    # small C and W over longer T: frequent evictions of branches, re-offers,
+    # deactivations and branch turns that close mid-chunk
+    _run_random(777, 300, T_max=60, B_max=3, C_max=6, W_max=10, ties=True)
+    _run_random(778, 150, T_max=60, B_max=2, C_max=40, W_max=6)

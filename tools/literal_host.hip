@@ -21,7 +21,7 @@ extern "C" int lit_decode_f32(const float* x, const int32_t* seq_len, int64_t Tm
   typedef float T;
   std::vector<char> lds(decode_lds_bytes(W, C, sizeof(T)) + 64);
   Ctx<T> cx;
-  carve(cx, lds.data(), W, (int)C);
+  carve(cx, lds.data(), W, W, (int)C);
   cx.blank = blank;
   std::vector<Rec> rec((size_t)Tmax * W);
   for (int64_t b = 0; b < B; ++b) {
