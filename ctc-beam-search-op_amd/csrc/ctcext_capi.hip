@@ -280,6 +280,9 @@ extern "C" int ctcext_decode(ctcext_decoder* d, const ctcext_decode_args* a, ctc
   // decoder.h:237-239 — raised by the first item's TopPaths
   if (B > 0 && a->top_paths > a->beam_width)
     return fail(CTCEXT_INVALID_ARGUMENT, "requested more paths than the beam width.");
+  if (B > 0 && C > ctcx::kMaxRecClasses)
+    return fail(CTCEXT_UNIMPLEMENTED, "num_classes " + std::to_string(C) + " exceeds the back-pointer record format (max " +
+                                          std::to_string(ctcx::kMaxRecClasses) + ")");
   if (B > 0 && a->beam_width > ctcext_max_beam_width(C, a->dtype))
     return fail(CTCEXT_UNIMPLEMENTED, "beam_width " + std::to_string(a->beam_width) + " with num_classes " +
                                           std::to_string(C) + " exceeds the LDS-resident beam state (max " +

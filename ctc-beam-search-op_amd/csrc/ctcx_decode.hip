@@ -1168,12 +1168,7 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
       sel(cx.flg, nx)[k] = fl;
       sel(cx.ot, nx)[k] = cx.et[e]; sel(cx.ob, nx)[k] = cx.eb[e]; sel(cx.ol, nx)[k] = cx.el[e];
       sel(cx.cb, nx)[k] = cx.ecb[e]; sel(cx.cn, nx)[k] = cx.ecn[e];
-      Rec rc;
-      rc.link = kd;
-      rc.label = cx.elab[e];
-      rc.bp_blank = (ef & F_HB) ? cx.ebpb[e] : kBpNone;
-      rc.bp_nblank = (ef & F_HN) ? cx.ebpn[e] : kBpNone;
-      rout[k] = rc;
+      rout[k] = rec_pack(kd, cx.elab[e], (ef & F_HB) ? cx.ebpb[e] : kBpNone, (ef & F_HN) ? cx.ebpn[e] : kBpNone);
     }
     __syncthreads();
     buf = nx;
@@ -1272,18 +1267,20 @@ __global__ __launch_bounds__(256) void ctcx_traceback(TraceParams tp) {
       int prev = -1;
       for (int t = sl - 1; t >= 0; --t) {
         const Rec r = rb[(int64_t)t * tp.W + k];
-        if (r.link & 1u) {
-          if (!tp.merge || r.label != prev) out[len++] = r.label;
-          prev = r.label;
+        const uint32_t link = rec_link(r);
+        if (link & 1u) {
+          const int lab = rec_label(r);
+          if (!tp.merge || lab != prev) out[len++] = lab;
+          prev = lab;
         }
-        k = (int)(r.link >> 1);
+        k = (int)(link >> 1);
       }
     } else {
       int kind = tp.top_kind[bp];
       for (int t = sl - 1; t >= 0 && kind >= 0; --t) {
         const Rec r = rb[(int64_t)t * tp.W + k];
-        out[len++] = kind == 0 ? tp.blank_label : r.label;
-        const uint32_t q = kind == 0 ? r.bp_blank : r.bp_nblank;
+        out[len++] = kind == 0 ? tp.blank_label : rec_label(r);
+        const uint32_t q = kind == 0 ? rec_bp_blank(r) : rec_bp_nblank(r);
         if (q >= kBpRestart) break;
         k = (int)(q >> 1);
         kind = (int)(q & 1u);

@@ -21,17 +21,32 @@ namespace ctcx {
 // events, 13 heap pushes (count)
 constexpr int kPhaseN = 16;
 
-// One record per (item, frame, surviving beam), written in the beam's sorted
-// position k (= its branch index next frame).  16 B so a lane stores it with
-// one dwordx4.  See DESIGN.md "records".
-struct Rec {
-  uint32_t link;    // (src branch << 1) | is_new_child  (prefix back-link)
-  int32_t label;    // the beam's last label (its prefix node's label)
-  uint32_t bp_blank;   // best blank-ending alignment candidate backpointer
-  uint32_t bp_nblank;  // best label-ending alignment candidate backpointer
-};
 constexpr uint32_t kBpRestart = 0xFFFFFFFEu;  // candidate started a new chain
 constexpr uint32_t kBpNone = 0xFFFFFFFFu;     // no candidate of that kind
+
+// One record per (item, frame, surviving beam), written in the beam's sorted
+// position k (= its branch index next frame): 8 bytes, packed
+//   bits  0..10  link = (src branch << 1) | is_new_child   (src < 512)
+//   bits 11..26  label + 1 (the beam's last label; -1 at the root)
+//   bits 27..38  best blank-ending alignment back-pointer (pos << 1 | kind),
+//   bits 39..50  best label-ending one; 4094 = restart, 4095 = none.
+// Valid for beam_width <= 512 and num_classes <= 65535 (both checked).
+typedef uint64_t Rec;
+__host__ __device__ inline uint64_t rec_bp12(uint32_t q) {
+  return q >= kBpRestart ? (uint64_t)(q - kBpRestart + 4094u) : (uint64_t)q;
+}
+__host__ __device__ inline uint32_t rec_unbp12(uint64_t v) {
+  return v >= 4094u ? kBpRestart + (uint32_t)(v - 4094u) : (uint32_t)v;
+}
+__host__ __device__ inline Rec rec_pack(uint32_t link, int label, uint32_t bp_blank, uint32_t bp_nblank) {
+  return (uint64_t)link | ((uint64_t)(uint32_t)(label + 1) << 11) | (rec_bp12(bp_blank) << 27) |
+         (rec_bp12(bp_nblank) << 39);
+}
+__host__ __device__ inline uint32_t rec_link(Rec r) { return (uint32_t)(r & 0x7FFu); }
+__host__ __device__ inline int rec_label(Rec r) { return (int)((r >> 11) & 0xFFFFu) - 1; }
+__host__ __device__ inline uint32_t rec_bp_blank(Rec r) { return rec_unbp12((r >> 27) & 0xFFFu); }
+__host__ __device__ inline uint32_t rec_bp_nblank(Rec r) { return rec_unbp12((r >> 39) & 0xFFFu); }
+constexpr int kMaxRecClasses = 65535;
 
 // Per-item results of the decode kernel.
 struct ItemOut {
