@@ -466,13 +466,38 @@ __device__ __forceinline__ HeapGeo<RN> heap_geo(int len, int dum_base) {
 // vpos >= 0 v is read from position vpos in the same LDS batch (pop_heap).
 // Returns the new root.
 template <typename T, int RN>
+struct HeapPairs {
+  HE<T> L[RN], R[RN];
+};
+
+// The sift's LDS reads (every lane's child pair), split off so that the push
+// loop can issue them before it selects the next event: they depend only on
+// the previous sift's stores, and their latency then overlaps the selection.
+template <typename T, int RN>
+__device__ __forceinline__ void heap_pairs(CTCX_LDS HE<T>* he, const HeapGeo<RN>& g, HeapPairs<T, RN>& hp) {
+#pragma unroll
+  for (int r = 0; r < RN; ++r) he_ld2(he, g.pair[r], hp.L[r], hp.R[r]);
+}
+
+template <typename T, int RN>
+__device__ __forceinline__ HE<T> wave_adjust_heap_p(CTCX_LDS HE<T>* he, const HeapGeo<RN>& g, HE<T> v,
+                                                    const HeapPairs<T, RN>& hp);
+
+template <typename T, int RN>
 __device__ __forceinline__ HE<T> wave_adjust_heap(CTCX_LDS HE<T>* he, const HeapGeo<RN>& g, HE<T> v,
                                                   int vpos = -1) {
-  const int lane = threadIdx.x;
   if (vpos >= 0) v = he_ld(he, uni(vpos) + 1);
-  HE<T> L[RN], R[RN];
-#pragma unroll
-  for (int r = 0; r < RN; ++r) he_ld2(he, g.pair[r], L[r], R[r]);
+  HeapPairs<T, RN> hp;
+  heap_pairs<T, RN>(he, g, hp);
+  return wave_adjust_heap_p<T, RN>(he, g, v, hp);
+}
+
+template <typename T, int RN>
+__device__ __forceinline__ HE<T> wave_adjust_heap_p(CTCX_LDS HE<T>* he, const HeapGeo<RN>& g, HE<T> v,
+                                                    const HeapPairs<T, RN>& hp) {
+  const int lane = threadIdx.x;
+  const HE<T>* L = hp.L;
+  const HE<T>* R = hp.R;
   T cv[RN];
   int cs[RN];
   unsigned pk[RN];
@@ -722,6 +747,8 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
         uint64_t liveM = __ballot(live), cevM = __ballot(cev);
         const HeapGeo<RN> geo = heap_geo<RN>(W, cx.wcap + 2);
         for (;;) {
+          HeapPairs<T, RN> hp;
+          heap_pairs<T, RN>(he, geo, hp);   // issued first: overlaps the event selection
 #ifdef CTCX_FASTLOOP_PROF
           const uint64_t q0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -754,13 +781,14 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
           const uint64_t q1 = __builtin_amdgcn_s_memtime();
 #endif
           const int fsl = front.s;
-          const bool evb = fsl < nb;
+          const int evbi = fsl < nb ? 1 : 0;
+          const bool evb = evbi != 0;
           int slot;
           if ((isbm >> k) & 1ull) {
             slot = bcast(c, k);
           } else {
             slot = evb ? nextfree : fsl;
-            nextfree += evb ? 1 : 0;
+            nextfree += evbi;
           }
           myslot = (myslot == fsl) ? -1 : myslot;
           evr = (evb && lane == nev) ? fsl : evr;
@@ -773,7 +801,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
 #ifdef CTCX_FASTLOOP_PROF
           const uint64_t q2 = __builtin_amdgcn_s_memtime();
 #endif
-          front = wave_adjust_heap<T, RN>(he, geo, nv);   // push = pop_heap(W + 1)
+          front = wave_adjust_heap_p<T, RN>(he, geo, nv, hp);   // push = pop_heap(W + 1)
           bottom = front.v;
           bat = (sl > k) ? bottom : bat;
 #ifdef CTCX_FASTLOOP_PROF
