@@ -1,0 +1,68 @@
+"""Generates tests/golden/large_vocab.json: oracle outputs for the large
+vocabulary configs of SURVEY.md 8(c) (cfg4-like C=1000/W=64 and cfg5-like
+C=5000/W=256, B=1), at lengths the CPU oracle finishes in seconds.
+
+The oracle is the CPU restatement in oracle/ (pinned by the reference golden
+test.py:20-100, see tests/test_oracle_golden.py); running it takes ~1 min
+here, so the outputs are committed and the GPU box only regenerates the
+inputs.  Inputs are NOT stored: they are float32 N(0,1) (distribution A,
+BASELINE.md) from numpy.random.default_rng(seed), shape [T, B, C], and the
+fixture records their sha256 so a numpy change that altered the stream would
+fail loudly instead of comparing against the wrong vectors.
+
+    python tests/golden/make_fixtures.py
+"""
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+# name: (seed, T, B, C, beam_width, top_paths, merge_repeated, blank_index, blank_label, seq_len)
+CASES = {
+    "cfg4_like_T100": (4001, 100, 1, 1000, 64, 1, False, 0, -1, [100]),
+    "cfg4_like_T60_B2_P3": (4002, 60, 2, 1000, 64, 3, True, 17, -1, [60, 41]),
+    "cfg5_like_T30": (5001, 30, 1, 5000, 256, 1, False, 0, -1, [30]),
+    "cfg5_like_T20_P2_blank_last": (5002, 20, 1, 5000, 256, 2, True, 4999, 4999, [20]),
+}
+
+
+def inputs(case):
+    seed, T, B, C = case[:4]
+    x = np.random.default_rng(seed).standard_normal((T, B, C), dtype=np.float32)
+    return x, np.asarray(case[9], np.int32)
+
+
+def sha(x):
+    return hashlib.sha256(np.ascontiguousarray(x).tobytes()).hexdigest()
+
+
+def main():
+    import oracle
+    out = {}
+    for name, case in CASES.items():
+        x, sl = inputs(case)
+        _, T, B, C, W, P, merge, blank, blabel, _ = case
+        r = oracle.decode(x, sl, W, P, merge_repeated=merge, blank_index=blank, blank_label=blabel)
+        out[name] = {
+            "case": list(case), "sha256": sha(x),
+            "decoded_indices": [np.asarray(v).tolist() for v in r.decoded_indices],
+            "decoded_values": [np.asarray(v).tolist() for v in r.decoded_values],
+            "decoded_shape": [np.asarray(v).tolist() for v in r.decoded_shape],
+            "alignment_indices": [np.asarray(v).tolist() for v in r.alignment_indices],
+            "alignment_values": [np.asarray(v).tolist() for v in r.alignment_values],
+            "alignment_shape": [np.asarray(v).tolist() for v in r.alignment_shape],
+            "log_probability_hex": [[float(v).hex() for v in row] for row in np.asarray(r.log_probability)],
+        }
+        print(name, "done", flush=True)
+    with open(os.path.join(HERE, "large_vocab.json"), "w") as f:
+        json.dump(out, f, separators=(",", ":"))
+
+
+if __name__ == "__main__":
+    main()

@@ -272,3 +272,30 @@ def test_random_reoffer_heavy():
     # deactivations and branch turns that close mid-chunk
     _run_random(777, 300, T_max=60, B_max=3, C_max=6, W_max=10, ties=True)
     _run_random(778, 150, T_max=60, B_max=2, C_max=40, W_max=6)
+
+
+# ---- large vocabularies (cfg4-like C=1000/W=64, cfg5-like
+# C=5000/W=256), against committed oracle outputs (tests/golden/make_fixtures.py)
+
+LARGE = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "large_vocab.json")))
+
+
+@pytest.mark.parametrize("name", sorted(LARGE))
+def test_large_vocab_golden(name):
+    import hashlib
+    import torch
+    fx = LARGE[name]
+    seed, T, B, C, W, P, merge, blank, blabel, sl = fx["case"]
+    x = np.random.default_rng(seed).standard_normal((T, B, C), dtype=np.float32)
+    assert hashlib.sha256(x.tobytes()).hexdigest() == fx["sha256"], "input stream changed"
+    out = ctcext_amd.ctc_ext_beam_search_decoder(
+        torch.as_tensor(x, device="cuda"), torch.as_tensor(np.asarray(sl, np.int32), device="cuda"),
+        W, P, merge_repeated=merge, blank_index=blank, blank_label=blabel)
+    for p in range(P):
+        for k in ("decoded_indices", "decoded_values", "decoded_shape",
+                  "alignment_indices", "alignment_values", "alignment_shape"):
+            got = to_numpy(getattr(out, k)[p])
+            exp = np.asarray(fx[k][p], np.int64)
+            np.testing.assert_array_equal(got.reshape(exp.shape), exp, err_msg="%s[%d]" % (k, p))
+    lp = np.asarray([[float.fromhex(h) for h in row] for row in fx["log_probability_hex"]], np.float32)
+    np.testing.assert_array_equal(to_numpy(out.log_probability), lp)
