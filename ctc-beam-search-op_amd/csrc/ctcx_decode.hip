@@ -1092,8 +1092,15 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
   int n_leaves = 1;
   __syncthreads();
 
+#ifdef CTCX_PHASES
+  // per-phase s_memtime accumulators (diagnostics builds only: the 16 live
+  // 64-bit counters cost the hot loops SGPRs)
   uint64_t pc[kPhaseN] = {};
   const bool prof = prm.prof != nullptr;
+#else
+  uint64_t pc[kPhaseN];
+  constexpr bool prof = false;
+#endif
   for (int t = 0; t < sl; ++t) {
     uint64_t t0 = prof ? __builtin_amdgcn_s_memtime() : 0;
     const T* xr = prm.x + ((int64_t)t * B + b) * C;

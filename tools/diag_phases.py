@@ -1,4 +1,9 @@
-"""Diagnostic: per-phase cycle split of ctcx_beam_decode (s_memtime stamps)."""
+"""Diagnostic: per-phase cycle split of ctcx_beam_decode (s_memtime stamps).
+
+Needs the counters build (the product library compiles them out):
+  make -C ctc-beam-search-op_amd/csrc phases
+  CTCEXT_LIB_PATH=$PWD/tools/libctcext_phases.so python tools/diag_phases.py B T W P [C]
+(add -DCTCX_FASTLOOP_PROF to the phases build for the per-event split)."""
 import ctypes, os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ctc-beam-search-op_amd"))
 import numpy as np
