@@ -552,6 +552,80 @@ __device__ __forceinline__ HE<T> wave_adjust_heap_p(CTCX_LDS HE<T>* he, const He
   return res;
 }
 
+// The HEAP_SORTED push, __adjust_heap(0, W, v) with the same decisions as
+// wave_adjust_heap_p, but without a scalar hand-off on its dependency chain:
+// the stop needs no find-first-set -- a path node is the stop iff it meets the
+// stop condition and none of its ancestors (a mask test against the second
+// ballot) does -- and the new root comes back in VGPRs (fv, fs: uniform
+// values), so the next event's compare reads it without a VALU -> SALU trip.
+// Requires g.nint > 0 (W >= 2).
+template <typename T, int RN>
+__device__ __forceinline__ void wave_push_heap_v(CTCX_LDS HE<T>* he, const HeapGeo<RN>& g, T vv, int vs,
+                                                 const HeapPairs<T, RN>& hp, T& fv, int& fs) {
+  const int lane = threadIdx.x;
+  if (g.nint == 0) {   // a heap of one: v is the root (uniform branch)
+    he_st(he, lane == 0 ? 1 : g.dum, HE<T>{vv, vs});
+    fv = vv;
+    fs = vs;
+    return;
+  }
+  const HE<T>* L = hp.L;
+  const HE<T>* R = hp.R;
+  T cv[RN];
+  int cs[RN];
+  unsigned pk[RN];
+  uint64_t bm[RN];
+#pragma unroll
+  for (int r = 0; r < RN; ++r) {
+    const bool pick_r = g.has_r[r] && !(R[r].v > L[r].v);
+    bm[r] = __ballot(pick_r);
+    pk[r] = pick_r ? 1u : 0u;
+    cv[r] = pick_r ? R[r].v : L[r].v;
+    cs[r] = pick_r ? R[r].s : L[r].s;
+  }
+  const T c0 = bcast(cv[0], 0);
+  const int s0 = bcast(cs[0], 0);
+  uint64_t cm[RN];
+  bool onp[RN], gtv[RN], cnd[RN];
+#pragma unroll
+  for (int r = 0; r < RN; ++r) {
+    unsigned mis;
+    if (RN == 1) {
+      mis = ((unsigned)bm[0] ^ g.req[r]) & g.anc[r];
+    } else {
+      mis = 0;
+#pragma unroll
+      for (int w = 0; w < (RN > 1 ? RN / 2 : 1); ++w)
+        mis |= ((bm[w] ^ g.req_w[r][w]) & g.anc_w[r][w]) != 0ull ? 1u : 0u;
+    }
+    onp[r] = (mis | g.off[r]) == 0u;
+    gtv[r] = cv[r] > vv;
+    const unsigned leaf = pk[r] ? g.leaf_r[r] : g.leaf_l[r];
+    cnd[r] = gtv[r] || leaf != 0u;
+    cm[r] = __ballot(onp[r] && cnd[r]);
+  }
+#pragma unroll
+  for (int r = 0; r < RN; ++r) {
+    bool above;   // a proper ancestor on the path already meets the stop condition
+    if (RN == 1) {
+      above = ((unsigned)cm[0] & g.anc[r]) != 0u;
+    } else {
+      above = false;
+#pragma unroll
+      for (int w = 0; w < (RN > 1 ? RN / 2 : 1); ++w) above |= (cm[w] & g.anc_w[r][w]) != 0ull;
+    }
+    const int j = r * 64 + lane;
+    const bool live = onp[r] && !above;
+    const bool up = live && !gtv[r];   // takes its min child (above the stop, or the stop with v below it)
+    const bool isk = live && cnd[r];   // the stop: v lands here or in its min child's position
+    he_st(he, up ? j + 1 : g.dum, HE<T>{cv[r], cs[r]});
+    he_st(he, isk ? (gtv[r] ? j : 2 * j + 1 + (int)pk[r]) + 1 : g.dum, HE<T>{vv, vs});
+  }
+  const bool keep = c0 > vv;
+  fv = keep ? vv : c0;
+  fs = keep ? vs : s0;
+}
+
 // peek_bottom() in the UNORDERED state: the first minimum moves to the front.
 // Returns the new front.
 template <typename T>
@@ -746,17 +820,23 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
         // compare per event feeds both decisions.
         uint64_t liveM = __ballot(live), cevM = __ballot(cev);
         const HeapGeo<RN> geo = heap_geo<RN>(W, cx.wcap + 2);
+        // the front and the bump pointer as (uniform) VGPR values: nothing on
+        // the event chain below leaves the vector unit except the event pick
+        T fv = front.v;
+        int fs = front.s;
+        int nfree = nextfree;
         for (;;) {
           HeapPairs<T, RN> hp;
           heap_pairs<T, RN>(he, geo, hp);   // issued first: overlaps the event selection
 #ifdef CTCX_FASTLOOP_PROF
           const uint64_t q0 = __builtin_amdgcn_s_memtime();
 #endif
-          const uint64_t gtM = __ballot(s > bottom);
+          const uint64_t gtM = __ballot(s > fv);
           const uint64_t m = liveM & ((isbm & cevM) | (~isbm & gtM)) & ~done;
           if (m == 0) break;
           const int k = (int)__builtin_ctzll(m);
-          if ((isbm >> k) & 1ull) {
+          const bool kbc = (isbm >> k) & 1ull;
+          if (__builtin_expect(kbc, 0)) {
             // only a re-offer can make a closed turn visible (a closed branch's new
             // children score <= its total <= bottom): was k's turn skipped?
             const uint64_t closedM = __ballot(!(bt > bat));
@@ -766,49 +846,45 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
               stop = true;
               continue;
             }
+            if (!((gtM >> k) & 1ull)) {
+              done = m ^ (m - 1ull);
+              const int k_c = bcast(c, k);
+              // re-offered evicted branch rejected -> deactivated (decoder.h:200-205)
+              evr = (lane == nev) ? (k_c | kDeactRec) : evr;
+              nev += 1;
+              liveM &= ~__ballot(i == k_c);
+              continue;
+            }
           }
           done = m ^ (m - 1ull);   // lanes <= k (k is m's lowest set bit; done's lanes are below it)
           const T k_s = bcast(s, k);
-          if (((isbm & ~gtM) >> k) & 1ull) {
-            const int k_c = bcast(c, k);
-            // re-offered evicted branch rejected -> deactivated (decoder.h:200-205)
-            evr = (lane == nev) ? (k_c | kDeactRec) : evr;
-            nev += 1;
-            liveM &= ~__ballot(i == k_c);
-            continue;
-          }
 #ifdef CTCX_FASTLOOP_PROF
           const uint64_t q1 = __builtin_amdgcn_s_memtime();
 #endif
-          const int fsl = front.s;
-          const int evbi = fsl < nb ? 1 : 0;
-          const bool evb = evbi != 0;
-          int slot;
-          if ((isbm >> k) & 1ull) {
-            slot = bcast(c, k);
-          } else {
-            slot = evb ? nextfree : fsl;
-            nextfree += evbi;
-          }
-          myslot = (myslot == fsl) ? -1 : myslot;
-          evr = (evb && lane == nev) ? fsl : evr;
+          // the evicted front: a branch's entry is reset and flagged (the slot
+          // stays the branch's); a new child's slot is reused
+          const bool evb = fs < nb;
+          const int slot = kbc ? bcast(c, k) : (evb ? nfree : fs);
+          nfree += (!kbc && evb) ? 1 : 0;
+          myslot = (myslot == fs) ? -1 : myslot;
+          evr = (evb && lane == nev) ? fs : evr;
           nev += evb ? 1 : 0;
           myslot = (lane == k) ? slot : myslot;
-          cevM |= isbm & __ballot(evb && c == fsl);
-          HE<T> nv;
-          nv.v = k_s;
-          nv.s = slot;
+          cevM |= isbm & __ballot(evb && c == fs);
 #ifdef CTCX_FASTLOOP_PROF
           const uint64_t q2 = __builtin_amdgcn_s_memtime();
 #endif
-          front = wave_adjust_heap_p<T, RN>(he, geo, nv, hp);   // push = pop_heap(W + 1)
-          bottom = front.v;
-          bat = (sl > k) ? bottom : bat;
+          wave_push_heap_v<T, RN>(he, geo, k_s, slot, hp, fv, fs);   // push = pop_heap(W + 1)
+          bat = (sl > k) ? fv : bat;
 #ifdef CTCX_FASTLOOP_PROF
           const uint64_t q3 = __builtin_amdgcn_s_memtime();
           if (pc) { pc[10] += q1 - q0; pc[12] += q2 - q1; pc[13] += q3 - q2; pc[6] += 1; }
 #endif
         }
+        front.v = uni(fv);
+        front.s = uni(fs);
+        bottom = front.v;
+        nextfree = uni(nfree);
         live = (liveM >> lane) & 1ull;
         cev = (cevM >> lane) & 1ull;
         break;
@@ -929,10 +1005,17 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
   int nout;
   if (st == kTopHeap) {
     // pop_heap(len): e[len-1] <- e[0], then sift the old e[len-1] from the root
+    T fv = front.v;
+    int fs = front.s;
     for (int len = W; len > 1; --len) {
-      const HE<T> old_front = front;
-      front = wave_adjust_heap<T, RN>(he, heap_geo<RN>(len - 1, cx.wcap + 2), front, len - 1);
-      if (lane == 0) he_st(he, len, old_front);
+      const HeapGeo<RN> geo = heap_geo<RN>(len - 1, cx.wcap + 2);
+      const HE<T> v = he_ld(he, len);   // e[len-1], read before the old front lands there
+      HeapPairs<T, RN> hp;
+      heap_pairs<T, RN>(he, geo, hp);
+      const T ofv = fv;
+      const int ofs = fs;
+      wave_push_heap_v<T, RN>(he, geo, v.v, v.s, hp, fv, fs);
+      if (lane == 0) he_st(he, len, HE<T>{ofv, ofs});
     }
     nout = W;
     for (int k = lane; k < nout; k += 64) cx.sorted[k] = he[k + 1].s;
