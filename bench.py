@@ -109,9 +109,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs for a one-GPU box (the driver's runs use neither):
+    # CTCX_ONE_DEVICE=1 puts every rank on cuda:0, CTCX_DIST_BACKEND=gloo
+    # replaces RCCL (which refuses two ranks on one device)
+    if os.environ.get("CTCX_ONE_DEVICE") == "1":
+        local = 0
+    backend = os.environ.get("CTCX_DIST_BACKEND", "nccl")
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -175,7 +184,8 @@ def main():
         "config": {"workload": args.config, "global_batch": B * world, "batch_per_gpu": B,
                    "seq_len": T, "num_classes": C, "beam_width": W, "top_paths": P,
                    "merge_repeated": merge, "parallelism": "batch-shard x%d" % world,
-                   "gather": world > 1 and not args.no_gather},
+                   "gather": world > 1 and not args.no_gather,
+                   "backend": ("rccl" if backend == "nccl" else backend) if world > 1 else None},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "ctcx_beam_decode", "kernel_ms": kavg,
