@@ -8,7 +8,7 @@
 //   ctcx_row_norm     one thread per (t, b) row: softmax normaliser, sequential
 //                     glibc-exact expf sum (decoder.h:72-80).
 //   ctcx_beam_decode  one wave64 workgroup per batch item, persistent over t.
-//                     Beam state lives in LDS; per frame it writes one 16-byte
+//                     Beam state lives in LDS; per frame it writes one 8-byte
 //                     record per surviving beam (prefix back-link + alignment
 //                     backpointers) to HBM.
 //   ctcx_traceback    one thread per (item, path, {decoded, alignment}): walks
