@@ -97,6 +97,7 @@ def main():
     ap.add_argument("--cpu-tcap", type=int, default=1500)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--no-host-io", action="store_true", help="skip the host-I/O (PCIe-inclusive) extra")
     ap.add_argument("--seq-len", type=int, default=0, help="diagnostics: override T (not a bench line)")
     args = ap.parse_args()
 
@@ -192,6 +193,20 @@ def main():
                      "algorithmic_bytes_per_launch": abytes},
         "literal_frames_per_step": lit / max(args.steps, 1),
     }
+    if world == 1 and not args.no_host_io:
+        # SURVEY 8(d)'s end-to-end form, never `value`: host logits in (one PCIe
+        # upload), SparseTensor components and log-probabilities back as host
+        # numpy arrays; timed outside the region above
+        ctcext_amd.ctc_ext_beam_search_decoder(x_np, sl_np, W, P, merge_repeated=merge,
+                                               blank_index=blank, blank_label=-1)
+        n_io = 2
+        t1 = time.perf_counter()
+        for _ in range(n_io):
+            ctcext_amd.ctc_ext_beam_search_decoder(x_np, sl_np, W, P, merge_repeated=merge,
+                                                   blank_index=blank, blank_label=-1)
+        io_s = (time.perf_counter() - t1) / n_io
+        res["host_io"] = {"frames_per_s": int(sl_np.sum()) / io_s, "ms_per_step": 1e3 * io_s,
+                          "steps": n_io, "what": "host numpy logits in, host numpy outputs out (PCIe both ways)"}
     if rank == 0 and world == 1 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_workers, args.cpu_tcap)
         res["cpu_baseline"]["gpu_over_cpu"] = value / res["cpu_baseline"]["value"]
