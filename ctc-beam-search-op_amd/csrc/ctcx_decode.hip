@@ -180,6 +180,12 @@ struct Ctx {
   int W, C, blank, enc, hts, wcap;
 };
 
+// Per-64-label block maxima of the logit row, right after the row (large C).
+template <typename T>
+__host__ __device__ __forceinline__ CTCX_LDS T* row_bmax(const Ctx<T>& cx) {
+  return (CTCX_LDS T*)((CTCX_LDS char*)cx.row + (((size_t)cx.C * sizeof(T) + 15) & ~(size_t)15));
+}
+
 // Frame-parity buffer select without indexing the pointer pair, so Ctx stays
 // in registers (a runtime index into a member array would force it to scratch).
 template <typename P>
@@ -665,7 +671,7 @@ __device__ HE<T> wave_first_min_to_front(CTCX_LDS HE<T>* he, int n) {
 // then peeks lazily; rare: only while the beam is still filling).
 // On success cx.sorted[0..*n_out) holds the Extract() order and, for the last
 // frame, cx.tops[0..min(P, leaves)) the TopPaths() selection as positions.
-template <typename T, int RN>
+template <typename T, int RN, bool BIG>
 __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, bool last, int P, int* n_out,
                           int* n_leaves, uint64_t* pc) {
   uint64_t ts0 = pc ? __builtin_amdgcn_s_memtime() : 0;
@@ -678,10 +684,24 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
 
   bool bad = !(norm > NI && norm < pinf<T>());
   T xmax = NI;
-  for (int j = lane; j < C; j += 64) {
-    const T xv = cx.row[j];
-    bad |= (xv != xv) || (xv == pinf<T>());
-    xmax = xv > xmax ? xv : xmax;
+  // large C: per 64-label block maxima of the row (bounds for window skipping
+  // in the grow loop below), stored after the row
+  CTCX_LDS T* bmax = row_bmax(cx);
+  if constexpr (BIG) {   // BIG <=> C > 64
+    for (int k = 0; k * 64 < C; ++k) {
+      const int j = k * 64 + lane;
+      const T xv = j < C ? cx.row[j] : NI;
+      bad |= (xv != xv) || (xv == pinf<T>());
+      xmax = xv > xmax ? xv : xmax;
+      const T bm = wave_max(xv);
+      if (lane == 0) bmax[k] = bm;
+    }
+  } else {
+    for (int j = lane; j < C; j += 64) {
+      const T xv = cx.row[j];
+      bad |= (xv != xv) || (xv == pinf<T>());
+      xmax = xv > xmax ? xv : xmax;
+    }
   }
   if (__ballot(bad)) return 1;
   // max_l (x_l - norm): float rounding is monotone, so pmax + base bounds
@@ -756,10 +776,37 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       const T ot0 = sel(cx.ot, buf)[i0];
       if (li0 == 0 && uni((int)!(ot0 > bottom))) break;   // branch i0's turn: skipped, and all later
       // (small C: a branch spans few chunks, and the chunk test below suffices)
-      if (Cm1 >= 64 && uni((int)(!(pmax + ot0 > bottom) && cx.bloom[i0] == 0ull))) {
-        ++i0;
+      if (!BIG && Cm1 >= 64 && uni((int)(!(pmax + ot0 > bottom) && cx.bloom[i0] == 0ull))) {
+        ++i0;   // (unreachable: C <= 64 here; kept so the small-C loop compiles as before)
         li0 = 0;
         continue;
+      }
+      if (BIG && uni((int)(cx.bloom[i0] == 0ull))) {
+        if (uni((int)!(pmax + ot0 > bottom))) {
+          ++i0;
+          li0 = 0;
+          continue;
+        }
+        // the branch's 64-offer windows one at a time: a window whose labels'
+        // block maxima bound every score (xb - norm) + ot0 <= bottom holds no
+        // accepted offer and no re-offer (bloom clear), so it is passed over
+        // (the same exact skip as the chunk test below, at two LDS reads)
+        bool rest = false;
+        for (;;) {
+          const int le = (li0 + 64 < Cm1 ? li0 + 64 : Cm1) - 1;
+          const int la = li0 + (li0 >= blank ? 1 : 0);
+          const int lb = le + (le >= blank ? 1 : 0);
+          const T ba = bmax[la >> 6], bb = bmax[lb >> 6];
+          const T xb = ba > bb ? ba : bb;
+          if (uni((int)(((xb - norm) + ot0) > bottom))) break;
+          if (li0 + 64 >= Cm1) { rest = true; break; }
+          li0 += 64;
+        }
+        if (rest) {
+          ++i0;
+          li0 = 0;
+          continue;
+        }
       }
     }
     const uint64_t tc0 = pc ? __builtin_amdgcn_s_memtime() : 0;
@@ -1145,7 +1192,7 @@ __host__ __device__ __attribute__((noinline)) int literal_step(Ctx<T> cx, int bu
 }
 
 // ---------------------------------------------------------------------------
-template <typename T, int RN, int WC>
+template <typename T, int RN, int WC, bool BIG>
 __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   Ctx<T> cx;
@@ -1197,7 +1244,7 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     int nl_fast = 0;
     uint64_t t1 = prof ? __builtin_amdgcn_s_memtime() : 0;
     if (prof) pc[0] += t1 - t0;
-    if (!prm.force_literal) why = exact_step<T, RN>(cx, buf, nb, norm, last, prm.P, &n, &nl_fast, prof ? pc : nullptr);
+    if (!prm.force_literal) why = exact_step<T, RN, BIG>(cx, buf, nb, norm, last, prm.P, &n, &nl_fast, prof ? pc : nullptr);
     __syncthreads();
     uint64_t t2 = prof ? __builtin_amdgcn_s_memtime() : 0;
     const bool ok = (why == 0);
@@ -1465,16 +1512,24 @@ __global__ __launch_bounds__(64) void ctcx_pack(PackParams pp) {
 // Launchers (called by the C-ABI layer).
 namespace ctcx {
 
-template <typename T, int RN, int WC>
-static hipError_t launch_decode_r(const DecodeParams<T>& p, hipStream_t s) {
+template <typename T, int RN, int WC, bool BIG>
+static hipError_t launch_decode_c(const DecodeParams<T>& p, hipStream_t s) {
   const size_t lds = decode_lds_bytes(WC > 0 ? WC : p.W, p.C, (int)sizeof(T));
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)ctcx_beam_decode<T, RN, WC>,
+    hipError_t e = hipFuncSetAttribute((const void*)ctcx_beam_decode<T, RN, WC, BIG>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((ctcx_beam_decode<T, RN, WC>), dim3((unsigned)p.B), dim3(64), lds, s, p);
+  hipLaunchKernelGGL((ctcx_beam_decode<T, RN, WC, BIG>), dim3((unsigned)p.B), dim3(64), lds, s, p);
   return hipGetLastError();
+}
+
+// BIG (C > 64): the grow loop's branch/window skipping by row-block maxima is
+// compiled in; small-C builds keep the leaner loop (its register allocation is
+// what cfg3 runs on)
+template <typename T, int RN, int WC>
+static hipError_t launch_decode_r(const DecodeParams<T>& p, hipStream_t s) {
+  return p.C > 64 ? launch_decode_c<T, RN, WC, true>(p, s) : launch_decode_c<T, RN, WC, false>(p, s);
 }
 
 template <typename T>

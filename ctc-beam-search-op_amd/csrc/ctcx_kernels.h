@@ -127,6 +127,7 @@ __host__ __device__ inline size_t decode_lds_bytes(int W, int64_t C, int tsize) 
   s += a16(8 * (size_t)W);                      // per-branch evicted-child label bloom
   s += ((size_t)W + 2 + 64) * (tsize == 8 ? 16 : 8); // TopN elements (value, slot) + per-lane dummy slots
   s += a16((size_t)C * tsize);                  // logit row
+  s += a16((size_t)((C + 63) / 64) * tsize);    // its per-64-label block maxima
   return s;
 }
 
