@@ -772,7 +772,69 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
   int i0 = 0, li0 = 0;   // the chunk's first offer: branch i0, label index li0
   bool stop = false;
   while (i0 < nb && !stop) {
-    if (full && (li0 == 0 || Cm1 >= 64)) {
+    if (BIG && full) {
+      // large C, lane-parallel: lane j tests branch i0 + j (its turn skipped:
+      // stop; its rest skippable whole: pmax + ot <= bottom, bloom clear), and
+      // the first branch that is neither skipped is where the scan resumes
+      // (the same per-branch tests, in the same order, 64 at a time)
+      int res = 0;   // 0: at a branch to scan, 1: a turn is skipped (stop), 2: past the last branch
+      for (;;) {
+        const int ib = i0 + lane;
+        bool brk = false, skp = true;
+        if (ib < nb) {
+          const T otb = sel(cx.ot, buf)[ib];
+          brk = (lane > 0 || li0 == 0) && !(otb > bottom);
+          skp = !(pmax + otb > bottom) && cx.bloom[ib] == 0ull;
+        }
+        const uint64_t hitM = __ballot(brk || !skp);
+        if (hitM == 0) {
+          i0 += 64;
+          li0 = 0;
+          if (i0 >= nb) { res = 2; break; }
+          continue;
+        }
+        const int k = (int)__builtin_ctzll(hitM);
+        if (k > 0) li0 = 0;
+        i0 += k;
+        if ((__ballot(brk) >> k) & 1ull) res = 1;
+        break;
+      }
+      if (res == 1) break;
+      if (res == 2) continue;
+      if (uni((int)(cx.bloom[i0] == 0ull))) {
+        // the branch's 64-offer windows, 64 windows per step (lane j: window
+        // li0 + 64 j): a window whose labels' block maxima bound every score
+        // (xb - norm) + ot0 <= bottom holds no accepted offer and no re-offer
+        // (bloom clear), so it is passed over (the chunk test below, at two
+        // LDS reads)
+        const T ot0 = sel(cx.ot, buf)[i0];
+        bool rest = false;
+        for (;;) {
+          const int lw = li0 + 64 * lane;
+          bool keep = false;
+          if (lw < Cm1) {
+            const int le = (lw + 64 < Cm1 ? lw + 64 : Cm1) - 1;
+            const int la = lw + (lw >= blank ? 1 : 0);
+            const int lb = le + (le >= blank ? 1 : 0);
+            const T ba = bmax[la >> 6], bb = bmax[lb >> 6];
+            const T xb = ba > bb ? ba : bb;
+            keep = ((xb - norm) + ot0) > bottom;
+          }
+          const uint64_t keepM = __ballot(keep);
+          if (keepM) {
+            li0 += 64 * (int)__builtin_ctzll(keepM);
+            break;
+          }
+          if (li0 + 64 * 64 >= Cm1) { rest = true; break; }
+          li0 += 64 * 64;
+        }
+        if (rest) {
+          ++i0;
+          li0 = 0;
+          continue;
+        }
+      }
+    } else if (full && (li0 == 0 || Cm1 >= 64)) {
       const T ot0 = sel(cx.ot, buf)[i0];
       if (li0 == 0 && uni((int)!(ot0 > bottom))) break;   // branch i0's turn: skipped, and all later
       // (small C: a branch spans few chunks, and the chunk test below suffices)
@@ -780,33 +842,6 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
         ++i0;   // (unreachable: C <= 64 here; kept so the small-C loop compiles as before)
         li0 = 0;
         continue;
-      }
-      if (BIG && uni((int)(cx.bloom[i0] == 0ull))) {
-        if (uni((int)!(pmax + ot0 > bottom))) {
-          ++i0;
-          li0 = 0;
-          continue;
-        }
-        // the branch's 64-offer windows one at a time: a window whose labels'
-        // block maxima bound every score (xb - norm) + ot0 <= bottom holds no
-        // accepted offer and no re-offer (bloom clear), so it is passed over
-        // (the same exact skip as the chunk test below, at two LDS reads)
-        bool rest = false;
-        for (;;) {
-          const int le = (li0 + 64 < Cm1 ? li0 + 64 : Cm1) - 1;
-          const int la = li0 + (li0 >= blank ? 1 : 0);
-          const int lb = le + (le >= blank ? 1 : 0);
-          const T ba = bmax[la >> 6], bb = bmax[lb >> 6];
-          const T xb = ba > bb ? ba : bb;
-          if (uni((int)(((xb - norm) + ot0) > bottom))) break;
-          if (li0 + 64 >= Cm1) { rest = true; break; }
-          li0 += 64;
-        }
-        if (rest) {
-          ++i0;
-          li0 = 0;
-          continue;
-        }
       }
     }
     const uint64_t tc0 = pc ? __builtin_amdgcn_s_memtime() : 0;
