@@ -823,7 +823,24 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
           const uint64_t keepM = __ballot(keep);
           if (keepM) {
             li0 += 64 * (int)__builtin_ctzll(keepM);
-            break;
+            // within the kept window, the exact per-label bound
+            // (x_l - norm) + ot0 > bottom (>= the offer's score: ob <= ot):
+            // the chunk starts at the first label passing it, and a window
+            // where none passes is passed over as well
+            const int lx = li0 + lane;
+            bool hot = false;
+            if (lx < Cm1) {
+              const int l = lx + (lx >= blank ? 1 : 0);
+              hot = ((cx.row[l] - norm) + ot0) > bottom;
+            }
+            const uint64_t hotM = __ballot(hot);
+            if (hotM) {
+              li0 += (int)__builtin_ctzll(hotM);
+              break;
+            }
+            if (li0 + 64 >= Cm1) { rest = true; break; }
+            li0 += 64;
+            continue;
           }
           if (li0 + 64 * 64 >= Cm1) { rest = true; break; }
           li0 += 64 * 64;
