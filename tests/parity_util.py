@@ -33,13 +33,14 @@ def compare(out, ref, top_paths, lp_exact=True):
         np.testing.assert_allclose(lp, ref.log_probability, rtol=0, atol=1e-5)
 
 
-def random_case(rng, T_max=40, B_max=3, C_max=11, W_max=15, ties=False, neg_inf=False, dtype=np.float32):
+def random_case(rng, T_max=40, B_max=3, C_max=11, W_max=15, ties=False, neg_inf=False, dtype=np.float32,
+                C_min=2, scale=1.0):
     T = int(rng.integers(1, T_max + 1))
     B = int(rng.integers(1, B_max + 1))
-    C = int(rng.integers(2, C_max + 1))
+    C = int(rng.integers(C_min, C_max + 1))
     W = int(rng.integers(1, W_max + 1))
     P = int(rng.integers(1, W + 1))
-    x = rng.standard_normal((T, B, C)).astype(dtype)
+    x = (rng.standard_normal((T, B, C)) * scale).astype(dtype)
     if ties:
         x = (np.round(x * 2) / 2).astype(dtype)
     if neg_inf:

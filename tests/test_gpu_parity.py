@@ -274,6 +274,16 @@ def test_random_reoffer_heavy():
     _run_random(778, 150, T_max=60, B_max=2, C_max=40, W_max=6)
 
 
+def test_random_large_c_skips():
+    # C > 64 runs the large-C kernel (branch scan 64 branches per step, block-max
+    # window scan, per-label refinement); W > 64 makes the branch scan take more
+    # than one step; peaked rows (scale 4) make most branches and windows
+    # skippable, ties and small W make evictions and re-offers (bloom) frequent
+    _run_random(881, 25, T_max=40, B_max=2, C_min=65, C_max=400, W_max=150, scale=4.0)
+    _run_random(882, 25, T_max=40, B_max=2, C_min=65, C_max=300, W_max=8, ties=True)
+    _run_random(883, 15, T_max=30, B_max=2, C_min=65, C_max=200, W_max=100)
+
+
 # ---- large vocabularies (cfg4-like C=1000/W=64, cfg5-like
 # C=5000/W=256), against committed oracle outputs (tests/golden/make_fixtures.py)
 
