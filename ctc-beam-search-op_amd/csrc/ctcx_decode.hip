@@ -778,13 +778,17 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       // the first branch that is neither skipped is where the scan resumes
       // (the same per-branch tests, in the same order, 64 at a time)
       int res = 0;   // 0: at a branch to scan, 1: a turn is skipped (stop), 2: past the last branch
+      T ot0 = NI;    // the found branch's total and bloom state, read out of its lane
+      bool bz0 = false;
       for (;;) {
         const int ib = i0 + lane;
-        bool brk = false, skp = true;
+        bool brk = false, skp = true, bz = false;
+        T otb = NI;
         if (ib < nb) {
-          const T otb = sel(cx.ot, buf)[ib];
+          otb = sel(cx.ot, buf)[ib];
+          bz = cx.bloom[ib] == 0ull;
           brk = (lane > 0 || li0 == 0) && !(otb > bottom);
-          skp = !(pmax + otb > bottom) && cx.bloom[ib] == 0ull;
+          skp = !(pmax + otb > bottom) && bz;
         }
         const uint64_t hitM = __ballot(brk || !skp);
         if (hitM == 0) {
@@ -797,17 +801,18 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
         if (k > 0) li0 = 0;
         i0 += k;
         if ((__ballot(brk) >> k) & 1ull) res = 1;
+        bz0 = (__ballot(bz) >> k) & 1ull;
+        ot0 = bcast(otb, k);
         break;
       }
       if (res == 1) break;
       if (res == 2) continue;
-      if (uni((int)(cx.bloom[i0] == 0ull))) {
+      if (bz0) {
         // the branch's 64-offer windows, 64 windows per step (lane j: window
         // li0 + 64 j): a window whose labels' block maxima bound every score
         // (xb - norm) + ot0 <= bottom holds no accepted offer and no re-offer
         // (bloom clear), so it is passed over (the chunk test below, at two
         // LDS reads)
-        const T ot0 = sel(cx.ot, buf)[i0];
         bool rest = false;
         for (;;) {
           const int lw = li0 + 64 * lane;
