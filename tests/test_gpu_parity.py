@@ -282,6 +282,8 @@ def test_random_large_c_skips():
     _run_random(881, 25, T_max=40, B_max=2, C_min=65, C_max=400, W_max=150, scale=4.0)
     _run_random(882, 25, T_max=40, B_max=2, C_min=65, C_max=300, W_max=8, ties=True)
     _run_random(883, 15, T_max=30, B_max=2, C_min=65, C_max=200, W_max=100)
+    # the float64 large-C instantiation
+    _run_random(884, 10, T_max=30, B_max=2, C_min=65, C_max=300, W_max=80, scale=4.0, dtype=np.float64)
 
 
 # ---- large vocabularies (cfg4-like C=1000/W=64, cfg5-like
