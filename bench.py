@@ -5,9 +5,13 @@ B=256 items, T=1500 frames, C=29 classes, beam_width=128, top_paths=3,
 merge_repeated=True; float32 logits [T,B,C] ~ N(0,1) from
 numpy.random.default_rng(20251015) (rank r>0: seed 20251015+r), already in
 HBM when the timed region starts.  One step = one full decode call through the
-C ABI (row normaliser, beam decode, traceback, int64 SparseTensor components
-materialised in HBM) plus, for N>1, the RCCL gather of every rank's outputs to
-rank 0.  Weak scaling: the global batch is 256*N.
+C ABI -- row normaliser, beam decode, traceback, int64 SparseTensor components
+packed on the device and materialised on the host ("logits
+already resident on device, output SparseTensor components materialised on
+host") -- plus, for N>1, the RCCL gather of every rank's outputs to rank 0.
+Weak scaling: the global batch is 256*N.  Extras beside `value`: the same call
+with the components left in HBM (`device_outputs`) and with host logits in
+(`host_io`, PCIe both ways).
 
 Prints ONE JSON line on rank 0 (see the contract in the task statement), with
 a roofline object for the dominant kernel (ctcx_beam_decode, timed with HIP
@@ -37,12 +41,46 @@ CONFIGS = {
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-def make_inputs(cfg, rank):
+HOST_GEN_LIMIT = 4 << 30   # logits above 4 GiB (cfg5: 30.7 GB) are drawn on the device
+
+
+def make_inputs(cfg, rank, dev):
+    """float32 [T,B,C] N(0,1) logits (distribution A) and seq_len = T.  numpy's
+    default_rng(20251015 + rank) as BASELINE.md says; past HOST_GEN_LIMIT a
+    seeded torch generator on the device instead (cfg5's 30.7 GB would take
+    minutes of host time)."""
+    import torch
     B, T, C = cfg[0], cfg[1], cfg[2]
+    sl = np.full(B, T, dtype=np.int32)
+    if T * B * C * 4 > HOST_GEN_LIMIT:
+        g = torch.Generator(device=dev)
+        g.manual_seed(20251015 + rank)
+        return None, torch.randn((T, B, C), generator=g, device=dev, dtype=torch.float32), sl, "torch-device"
     rng = np.random.default_rng(20251015 + rank)
     x = rng.standard_normal((T, B, C), dtype=np.float32)
-    sl = np.full(B, T, dtype=np.int32)
-    return x, sl
+    return x, torch.as_tensor(x, device=dev), sl, "numpy"
+
+
+def lib_hash():
+    """sha256 of the libctcext.so this run loads (stamps the PMC traffic file)."""
+    import hashlib
+    from ctcext_amd import _lib
+    with open(_lib.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def cpu_share():
+    """CPUs this process may use: the affinity mask, bounded by a cgroup v2
+    quota when one is set (the GPU box's nproc shows the whole machine)."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return (min(n, quota) if quota else n), {"nproc": os.cpu_count(), "affinity": n, "cgroup_quota": quota}
 
 
 def algorithmic_bytes(sl, C, P, out, tsize=4):
@@ -65,7 +103,7 @@ def _cpu_worker(args):
 def cpu_baseline(cfg, n_workers, t_cap):
     """The oracle in reference-cost mode (per-candidate std::vector alignment
     copies, per-child heap nodes, TopN heap) on `n_workers` items of the
-    workload, one item per process — the reference op is single-threaded
+    workload, one item per process -- the reference op is single-threaded
     (kernels.cc:68), so one process per core is its all-cores form."""
     B, T, C, W, P, merge, blank = cfg
     T = min(T, t_cap)
@@ -93,8 +131,11 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
-    ap.add_argument("--cpu-workers", type=int, default=int(os.environ.get("CTCX_CPU_WORKERS", "16")))
-    ap.add_argument("--cpu-tcap", type=int, default=1500)
+    ap.add_argument("--cpu-workers", type=int, default=int(os.environ.get("CTCX_CPU_WORKERS", "0")),
+                    help="0: the CPU share of this process (affinity mask and cgroup quota)")
+    ap.add_argument("--cpu-tcap", type=int, default=0,
+                    help="frames per CPU-baseline item (0: the config's T, or 100 / 20 frames for cfg4 / "
+                         "cfg5, whose full items need ~48 GB / ~1.4 TB on the reference's CPU path)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-host-io", action="store_true", help="skip the host-I/O (PCIe-inclusive) extra")
@@ -129,20 +170,24 @@ def main():
     if args.seq_len:
         cfg = (cfg[0], args.seq_len) + cfg[2:]
     B, T, C, W, P, merge, blank = cfg
-    x_np, sl_np = make_inputs(cfg, rank)
-    x = torch.as_tensor(x_np, device=dev)
+    x_np, x, sl_np, gen = make_inputs(cfg, rank, dev)
     sl = torch.as_tensor(sl_np, device=dev)
     torch.cuda.synchronize()
 
     flags = _lib.CTCEXT_FLAG_PROFILE
     dec = ctcext_amd.get_decoder(local)
 
-    def step():
+    def step(outputs="host"):
+        # 8(d): device-resident logits in, SparseTensor components on the host
+        # out (world > 1: device outputs, gathered over RCCL to rank 0)
         out = ctcext_amd.ctc_ext_beam_search_decoder(x, sl, W, P, merge_repeated=merge,
-                                                     blank_index=blank, blank_label=-1, flags=flags)
+                                                     blank_index=blank, blank_label=-1, flags=flags,
+                                                     outputs=outputs if world == 1 else "device")
         if world > 1 and not args.no_gather:
-            gather_to_root(out, rank * B, P)
-        return out
+            got = gather_to_root(out, rank * B, P)
+            if got is not None:   # rank 0: the whole batch's components to the host
+                [[t.cpu() for t in f] if isinstance(f, list) else f.cpu() for f in got]
+        return out   # this rank's own decode (its algorithmic bytes)
 
     for _ in range(args.warmup):
         out = step()
@@ -173,27 +218,50 @@ def main():
     kavg = float(np.mean(kms))
     abytes = algorithmic_bytes(sl_np, C, P, out)
     achieved = abytes / (kavg * 1e-3) / 1e9
-    traffic = None
+    # HBM bytes per launch from this build's PMC passes (tools/pmc_summary.py);
+    # a file stamped with another library build is stale and not used
+    traffic, traffic_src = None, "no PMC file for this config"
     pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
     if os.path.exists(pmc):
-        traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        pj = json.load(open(pmc))
+        if pj.get("lib_sha16") == lib_hash() and pj.get("seq_len", T) == T:
+            traffic, traffic_src = pj.get("hbm_bytes_per_launch"), os.path.relpath(pmc, ROOT)
+        else:
+            traffic_src = "stale: %s is of build %s, this is %s" % (os.path.relpath(pmc, ROOT),
+                                                                   pj.get("lib_sha16"), lib_hash())
     res = {
         "metric": "decoded frames/sec at B=256, T=1500, C=29, beam_width=128; 1/2/4/8 GPUs",
         "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic N(0,1) logits (%s generator)" % gen,
         "config": {"workload": args.config, "global_batch": B * world, "batch_per_gpu": B,
                    "seq_len": T, "num_classes": C, "beam_width": W, "top_paths": P,
                    "merge_repeated": merge, "parallelism": "batch-shard x%d" % world,
                    "gather": world > 1 and not args.no_gather,
                    "backend": ("rccl" if backend == "nccl" else backend) if world > 1 else None},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "ctcx_beam_decode", "kernel_ms": kavg,
                      "algorithmic_bytes_per_launch": abytes},
         "literal_frames_per_step": lit / max(args.steps, 1),
+        "lib_sha16": lib_hash(),
+        "what": ("one decode call: device logits in, int64 SparseTensor components materialised on the host"
+                 if world == 1 else "one decode call per rank (device outputs) + RCCL gather to rank 0"),
     }
     if world == 1 and not args.no_host_io:
+        # the same call with the components left in HBM (no device->host copy)
+        n_dev = max(1, min(args.steps, 3))
+        step("device")
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(n_dev):
+            step("device")
+        torch.cuda.synchronize()
+        dv_s = (time.perf_counter() - t1) / n_dev
+        res["device_outputs"] = {"frames_per_s": int(sl_np.sum()) / dv_s, "ms_per_step": 1e3 * dv_s,
+                                 "steps": n_dev, "what": "device logits in, components left in HBM"}
+    if world == 1 and not args.no_host_io and x_np is not None:
         # SURVEY 8(d)'s end-to-end form, never `value`: host logits in (one PCIe
         # upload), SparseTensor components and log-probabilities back as host
         # numpy arrays; timed outside the region above
@@ -208,8 +276,14 @@ def main():
         res["host_io"] = {"frames_per_s": int(sl_np.sum()) / io_s, "ms_per_step": 1e3 * io_s,
                           "steps": n_io, "what": "host numpy logits in, host numpy outputs out (PCIe both ways)"}
     if rank == 0 and world == 1 and not args.no_cpu:
-        res["cpu_baseline"] = cpu_baseline(cfg, args.cpu_workers, args.cpu_tcap)
+        share, info = cpu_share()
+        nw = args.cpu_workers or share
+        tcap = args.cpu_tcap or {"cfg4": 100, "cfg5": 20}.get(args.config, T)
+        res["cpu_baseline"] = cpu_baseline(cfg, nw, tcap)
+        if tcap < T:
+            res["cpu_baseline"]["truncated"] = "T=%d of %d (BASELINE.md: full items do not fit host memory)" % (tcap, T)
         res["cpu_baseline"]["gpu_over_cpu"] = value / res["cpu_baseline"]["value"]
+        res["cpu_baseline"]["host_cpus"] = info
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

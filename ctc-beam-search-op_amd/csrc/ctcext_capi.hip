@@ -1,9 +1,10 @@
 // ctcext_capi.hip — host side of libctcext.so: validation, workspace, kernel
-// orchestration and output transfer behind the C ABI in include/ctcext.h.
+// orchestration, multi-device sharding and output transfer behind the C ABI
+// in include/ctcext.h.
 //
 // Mirrors the reference op kernel (cc/kernels/ctc_ext_beam_search_decoder_kernels.cc):
-//   ValidateInputsGenerateOutputs  :97-160  -> validate()
-//   Compute batch/time loop        :67-90   -> ctcx_row_norm + ctcx_beam_decode
+//   ValidateInputsGenerateOutputs  :97-139  -> validate_shapes / check_lengths (ctcext_validate)
+//   Compute batch/time loop        :67-90   -> ctcx_row_norm + ctcx_beam_decode per shard
 //   TopPaths errors                decoder.h:237-243
 //   StoreAllDecodedSequences       :163-257 -> ctcx_traceback + ctcx_scan + ctcx_pack
 #include <hip/hip_runtime.h>
@@ -11,6 +12,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -21,7 +23,8 @@ namespace ctcx {
 template <typename T>
 hipError_t launch_decode(const DecodeParams<T>& p, hipStream_t s);
 template <typename T>
-hipError_t launch_row_norm(const T* x, const int32_t* sl, T* norm, int64_t T_, int64_t B, int64_t C, hipStream_t s);
+hipError_t launch_row_norm(const T* x, const int32_t* sl, T* norm, int64_t T_, int64_t B, int64_t C,
+                           int64_t xstride, hipStream_t s);
 hipError_t launch_traceback(const TraceParams& tp, hipStream_t s);
 hipError_t launch_scan(const int32_t* len, int64_t* off, int64_t* res, int64_t B, int P, hipStream_t s);
 hipError_t launch_pack(const PackParams& pp, hipStream_t s);
@@ -43,6 +46,18 @@ static int fail(int code, const std::string& msg) {
   } while (0)
 
 namespace {
+
+// Restores the calling thread's current HIP device on every exit path: the
+// caller (e.g. torch in a per-rank process) reads the same runtime's device.
+struct DeviceGuard {
+  int prev = -1;
+  DeviceGuard() {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
 
 struct DevBuf {
   void* p = nullptr;
@@ -84,66 +99,103 @@ struct HostBuf {
   }
 };
 
+// One device of a handle: its stream, events and the per-shard workspace.
+// The root (devs[0]) also holds the whole batch's walks, lengths and outputs.
+struct Dev {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t s = nullptr;   // stream of the current call
+  hipEvent_t ev[4] = {};
+  DevBuf x, sl, norm, rec, item, top_pos, top_kind, logp, seq, len, phase;
+  int64_t lo = 0, nb = 0;    // this call's shard [lo, lo + nb)
+};
+
 }  // namespace
 
 struct ctcext_decoder {
-  int device = 0;
-  hipStream_t own_stream = nullptr;
-  // workspace
-  DevBuf x, sl, norm, rec, item, top_pos, top_kind, logp, seq, len, off, res, ptrs, out_idx, out_val, phase;
-  HostBuf h_item, h_res;
-  hipEvent_t ev[6] = {};
+  std::vector<Dev> devs;
+  // root-side: scan results and output staging
+  DevBuf off, res, ptrs, out_idx, out_val;
+  HostBuf h_item, h_res, h_kind;
   // state of the last successful decode (consumed by fetch)
   bool have = false;
   int dtype = 0;
   int64_t T = 0, B = 0, C = 0;
   int32_t W = 0, P = 0;
-  hipStream_t stream = nullptr;
   std::vector<ctcext_path_sizes> sizes;
   ctcext_stats stats{};
 };
 
-static size_t lds_limit() { return ctcx::kLdsBytes; }
+static void release_dev(Dev& d) {
+  (void)hipSetDevice(d.device);
+  if (d.own_stream) (void)hipStreamSynchronize(d.own_stream);
+  DevBuf* bufs[] = {&d.x, &d.sl, &d.norm, &d.rec, &d.item, &d.top_pos, &d.top_kind, &d.logp,
+                    &d.seq, &d.len, &d.phase};
+  for (DevBuf* b : bufs) b->release();
+  for (auto& ev : d.ev)
+    if (ev) (void)hipEventDestroy(ev);
+  if (d.own_stream) (void)hipStreamDestroy(d.own_stream);
+  d.own_stream = nullptr;
+}
 
 extern "C" int32_t ctcext_max_beam_width(int64_t num_classes, int32_t dtype) {
   const int ts = dtype == CTCEXT_F64 ? 8 : 4;
   int lo = 0;
   for (int w = 1; w <= 512; ++w)
-    if (ctcx::decode_lds_bytes(w, num_classes, ts) <= lds_limit()) lo = w;
+    if (ctcx::decode_lds_bytes(w, num_classes, ts) <= ctcx::kLdsBytes) lo = w;
   return lo;
 }
 
-extern "C" int ctcext_create(int device, ctcext_decoder** out) {
-  if (!out) return fail(CTCEXT_INVALID_ARGUMENT, "null output handle");
+extern "C" int ctcext_create_sharded(const int* devices, int n_devices, ctcext_decoder** out) {
+  if (!out || !devices || n_devices < 1) return fail(CTCEXT_INVALID_ARGUMENT, "null argument or no devices");
+  DeviceGuard guard;
   int n = 0;
   HIP_OR_FAIL(hipGetDeviceCount(&n));
-  if (device < 0 || device >= n) return fail(CTCEXT_INVALID_ARGUMENT, "invalid device ordinal");
-  HIP_OR_FAIL(hipSetDevice(device));
+  for (int i = 0; i < n_devices; ++i)
+    if (devices[i] < 0 || devices[i] >= n) return fail(CTCEXT_INVALID_ARGUMENT, "invalid device ordinal");
   ctcext_decoder* d = new ctcext_decoder();
-  d->device = device;
-  hipError_t e = hipStreamCreateWithFlags(&d->own_stream, hipStreamNonBlocking);
-  if (e != hipSuccess) {
-    delete d;
-    return fail(CTCEXT_INTERNAL, std::string("HIP error: ") + hipGetErrorString(e));
+  d->devs.resize((size_t)n_devices);
+  for (int i = 0; i < n_devices; ++i) {
+    Dev& v = d->devs[(size_t)i];
+    v.device = devices[i];
+    hipError_t e = hipSetDevice(v.device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&v.own_stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      for (int j = 0; j < i; ++j) release_dev(d->devs[(size_t)j]);
+      delete d;
+      return fail(CTCEXT_INTERNAL, std::string("HIP error: ") + hipGetErrorString(e));
+    }
+    for (auto& ev : v.ev) (void)hipEventCreate(&ev);
+    // the shard inputs and the gathered walks move between the root and this
+    // device by peer copies (xGMI); "already enabled" is fine
+    if (v.device != devices[0]) {
+      int ok = 0;
+      (void)hipDeviceCanAccessPeer(&ok, v.device, devices[0]);
+      if (ok) {
+        (void)hipDeviceEnablePeerAccess(devices[0], 0);
+        (void)hipSetDevice(devices[0]);
+        (void)hipDeviceEnablePeerAccess(v.device, 0);
+      }
+      (void)hipGetLastError();
+    }
   }
-  for (auto& ev : d->ev) (void)hipEventCreate(&ev);
   *out = d;
   g_err.clear();
   return CTCEXT_OK;
 }
 
+extern "C" int ctcext_create(int device, ctcext_decoder** out) { return ctcext_create_sharded(&device, 1, out); }
+
 extern "C" void ctcext_destroy(ctcext_decoder* d) {
   if (!d) return;
-  (void)hipSetDevice(d->device);
-  if (d->own_stream) (void)hipStreamSynchronize(d->own_stream);
-  DevBuf* bufs[] = {&d->x, &d->sl, &d->norm, &d->rec, &d->item, &d->top_pos, &d->top_kind, &d->logp,
-                    &d->seq, &d->len, &d->off, &d->res, &d->ptrs, &d->out_idx, &d->out_val, &d->phase};
+  DeviceGuard guard;
+  (void)hipSetDevice(d->devs[0].device);
+  DevBuf* bufs[] = {&d->off, &d->res, &d->ptrs, &d->out_idx, &d->out_val};
   for (DevBuf* b : bufs) b->release();
   d->h_item.release();
   d->h_res.release();
-  for (auto& ev : d->ev)
-    if (ev) (void)hipEventDestroy(ev);
-  if (d->own_stream) (void)hipStreamDestroy(d->own_stream);
+  d->h_kind.release();
+  for (Dev& v : d->devs) release_dev(v);
   delete d;
 }
 
@@ -151,117 +203,304 @@ extern "C" const char* ctcext_last_error(void) { return g_err.c_str(); }
 
 extern "C" int ctcext_phase_counters(ctcext_decoder* d, uint64_t* out, int64_t n) {
   if (!d || !out) return fail(CTCEXT_INVALID_ARGUMENT, "null argument");
-  if (!d->phase.p) return fail(CTCEXT_FAILED_PRECONDITION, "no CTCEXT_FLAG_PHASES decode yet");
-  if (n < 0 || 8 * (size_t)n > d->phase.cap) return fail(CTCEXT_INVALID_ARGUMENT, "n exceeds the counter buffer");
-  HIP_OR_FAIL(hipSetDevice(d->device));
-  HIP_OR_FAIL(hipMemcpy(out, d->phase.p, 8 * (size_t)n, hipMemcpyDeviceToHost));
+  Dev& r = d->devs[0];
+  if (!r.phase.p) return fail(CTCEXT_FAILED_PRECONDITION, "no CTCEXT_FLAG_PHASES decode yet");
+  if (n < 0 || 8 * (size_t)n > r.phase.cap) return fail(CTCEXT_INVALID_ARGUMENT, "n exceeds the counter buffer");
+  DeviceGuard guard;
+  HIP_OR_FAIL(hipSetDevice(r.device));
+  HIP_OR_FAIL(hipMemcpy(out, r.phase.p, 8 * (size_t)n, hipMemcpyDeviceToHost));
   return CTCEXT_OK;
 }
 
 extern "C" int ctcext_get_stats(ctcext_decoder* d, ctcext_stats* s) {
   if (!d || !s) return fail(CTCEXT_INVALID_ARGUMENT, "null argument");
   *s = d->stats;
+  s->n_devices = (int32_t)d->devs.size();
+  return CTCEXT_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Validation, in the reference's order (kernels.cc:97-139), host only.
+
+// The op definition's attribute constraints (ops.cc:10-17) and the input
+// shapes (kernels.cc:109-130).
+static int validate_shapes(const ctcext_decode_args* a) {
+  if (!a) return fail(CTCEXT_INVALID_ARGUMENT, "null argument");
+  if (a->dtype != CTCEXT_F32 && a->dtype != CTCEXT_F64)
+    return fail(CTCEXT_INVALID_ARGUMENT, "dtype must be float32 or float64");
+  if (a->beam_width < 1)
+    return fail(CTCEXT_INVALID_ARGUMENT, "Value for attr 'beam_width' of " + std::to_string(a->beam_width) +
+                                             " must be at least minimum 1");
+  if (a->top_paths < 1)
+    return fail(CTCEXT_INVALID_ARGUMENT, "Value for attr 'top_paths' of " + std::to_string(a->top_paths) +
+                                             " must be at least minimum 1");
+  if (a->inputs_dims != 3) return fail(CTCEXT_INVALID_ARGUMENT, "inputs is not a 3-Tensor");
+  const int64_t T_ = a->max_time, B = a->batch_size, C = a->num_classes;
+  if (T_ < 0 || B < 0 || C < 0) return fail(CTCEXT_INVALID_ARGUMENT, "inputs has a negative dimension");
+  if (T_ == 0) return fail(CTCEXT_INVALID_ARGUMENT, "max_time is 0");
+  if (a->sequence_length_dims != 1) return fail(CTCEXT_INVALID_ARGUMENT, "sequence_length is not a vector");
+  if (a->sequence_length_size != B)
+    return fail(CTCEXT_FAILED_PRECONDITION, "len(sequence_length) != batch_size.  len(sequence_length):  " +
+                                                std::to_string(a->sequence_length_size) +
+                                                " batch_size: " + std::to_string(B));
+  if (B > 0 && (!a->inputs || !a->sequence_length)) return fail(CTCEXT_INVALID_ARGUMENT, "null input pointer");
+  return CTCEXT_OK;
+}
+
+// kernels.cc:133-139
+static int check_lengths(const int32_t* hsl, int64_t B, int64_t T_) {
+  for (int64_t b = 0; b < B; ++b)
+    if (!(hsl[b] <= T_))
+      return fail(CTCEXT_FAILED_PRECONDITION, "sequence_length(" + std::to_string(b) + ") <= " + std::to_string(T_));
+  return CTCEXT_OK;
+}
+
+// What the reference leaves unchecked or raises per item, and this library's
+// own limits.
+static int check_limits(const ctcext_decode_args* a) {
+  const int64_t B = a->batch_size, C = a->num_classes;
+  if (B == 0) return CTCEXT_OK;
+  // the reference reads out of bounds here (no check); this library refuses
+  if (a->blank_index < 0 || a->blank_index >= C)
+    return fail(CTCEXT_INVALID_ARGUMENT, "blank_index out of range [0, num_classes)");
+  // decoder.h:237-239 — raised by the first item's TopPaths
+  if (a->top_paths > a->beam_width) return fail(CTCEXT_INVALID_ARGUMENT, "requested more paths than the beam width.");
+  if (C > ctcx::kMaxRecClasses)
+    return fail(CTCEXT_UNIMPLEMENTED, "num_classes " + std::to_string(C) +
+                                          " exceeds the back-pointer record format (max " +
+                                          std::to_string(ctcx::kMaxRecClasses) + ")");
+  const int wmax = ctcext_max_beam_width(C, a->dtype);
+  if (a->beam_width > wmax)
+    return fail(CTCEXT_UNIMPLEMENTED, "beam_width " + std::to_string(a->beam_width) + " with num_classes " +
+                                          std::to_string(C) + " exceeds the LDS-resident beam state (max " +
+                                          std::to_string(wmax) + ")");
+  return CTCEXT_OK;
+}
+
+extern "C" int ctcext_validate(const ctcext_decode_args* a) {
+  int rc = validate_shapes(a);
+  if (rc != CTCEXT_OK) return rc;
+  if (!a->inputs_on_device) {
+    rc = check_lengths(a->sequence_length, a->batch_size, a->max_time);
+    if (rc != CTCEXT_OK) return rc;
+  }
+  rc = check_limits(a);
+  if (rc == CTCEXT_OK) g_err.clear();
+  return rc;
+}
+
+// ---------------------------------------------------------------------------
+// Decode.
+
+// Contiguous shards balanced by sum(max(seq_len, 0)): shard i
+// ends at the first item whose running sum reaches (i + 1) / n of the total.
+static void shard_bounds(const std::vector<int32_t>& hsl, int n, std::vector<int64_t>& lo) {
+  const int64_t B = (int64_t)hsl.size();
+  lo.assign((size_t)n + 1, B);
+  lo[0] = 0;
+  int64_t tot = 0;
+  for (int32_t v : hsl) tot += v > 0 ? v : 0;
+  if (tot == 0) {   // no frames anywhere: split by count
+    for (int i = 1; i < n; ++i) lo[(size_t)i] = B * i / n;
+    return;
+  }
+  int64_t run = 0, b = 0;
+  for (int i = 1; i < n; ++i) {
+    const int64_t goal = (tot * i + n - 1) / n;
+    while (b < B && run < goal) {
+      const int32_t v = hsl[(size_t)b];
+      run += v > 0 ? v : 0;
+      ++b;
+    }
+    lo[(size_t)i] = b;
+  }
+}
+
+// Enqueues norm + decode + traceback of one shard on its device's stream.
+// x/sl point at the shard's first item; xstride is items per frame in x.
+template <typename T>
+static int enqueue_shard(ctcext_decoder* d, Dev& v, bool root, const ctcext_decode_args* a, const T* x,
+                         int64_t xstride, const int32_t* sl) {
+  const int64_t T_ = a->max_time, C = a->num_classes, B = d->B, Bs = v.nb;
+  const int W = a->beam_width, P = a->top_paths;
+  const bool prof = (a->flags & CTCEXT_FLAG_PROFILE) != 0;
+  const int64_t Bo = root ? B : Bs;   // the root's walk buffers hold the whole batch
+  hipStream_t s = v.s;
+  HIP_OR_FAIL(v.norm.ensure(sizeof(T) * (size_t)(T_ * Bs)));
+  HIP_OR_FAIL(v.rec.ensure(sizeof(ctcx::Rec) * (size_t)(Bs * T_ * W)));
+  HIP_OR_FAIL(v.item.ensure(sizeof(ctcx::ItemOut) * (size_t)Bo));
+  HIP_OR_FAIL(v.top_pos.ensure(4 * (size_t)(Bs * P)));
+  HIP_OR_FAIL(v.top_kind.ensure(4 * (size_t)(Bo * P)));
+  HIP_OR_FAIL(v.logp.ensure(sizeof(T) * (size_t)(Bo * P)));
+  HIP_OR_FAIL(v.seq.ensure(4 * (size_t)(Bo * P * 2 * T_)));
+  HIP_OR_FAIL(v.len.ensure(4 * (size_t)(Bo * P * 2)));
+
+  if (prof) HIP_OR_FAIL(hipEventRecord(v.ev[0], s));
+  HIP_OR_FAIL(ctcx::launch_row_norm<T>(x, sl, (T*)v.norm.p, T_, Bs, C, xstride, s));
+  if (prof) HIP_OR_FAIL(hipEventRecord(v.ev[1], s));
+
+  ctcx::DecodeParams<T> p{};
+  p.x = x;
+  p.norm = (const T*)v.norm.p;
+  p.seq_len = sl;
+  p.Tmax = T_; p.B = Bs; p.C = C; p.xstride = xstride;
+  p.W = W; p.P = P; p.blank = a->blank_index; p.blank_label = a->blank_label;
+  p.force_literal = (a->flags & CTCEXT_FLAG_FORCE_LITERAL) ? 1 : 0;
+  p.rec = (ctcx::Rec*)v.rec.p;
+  p.item = (ctcx::ItemOut*)v.item.p;
+  p.top_pos = (int32_t*)v.top_pos.p;
+  p.top_kind = (int32_t*)v.top_kind.p;
+  p.log_prob = (T*)v.logp.p;
+  p.prof = nullptr;
+  if (a->flags & CTCEXT_FLAG_PHASES) {
+    HIP_OR_FAIL(v.phase.ensure(8 * ctcx::kPhaseN * (size_t)Bs));
+    p.prof = (uint64_t*)v.phase.p;
+  }
+  // the host checked the shapes the kernel's grid and LDS carve assume
+  if (Bs > 0x7fffffffLL || W > 512 || C > ctcx::kMaxRecClasses)
+    return fail(CTCEXT_INTERNAL, "shard shape outside the kernel's limits");
+  HIP_OR_FAIL(ctcx::launch_decode<T>(p, s));
+  if (prof) HIP_OR_FAIL(hipEventRecord(v.ev[2], s));
+
+  ctcx::TraceParams tp{};
+  tp.rec = p.rec; tp.item = p.item; tp.seq_len = sl; tp.top_pos = p.top_pos; tp.top_kind = p.top_kind;
+  tp.Tmax = T_; tp.B = Bs; tp.W = W; tp.P = P; tp.merge = a->merge_repeated ? 1 : 0;
+  tp.blank_label = a->blank_label;
+  tp.seq = (int32_t*)v.seq.p;
+  tp.len = (int32_t*)v.len.p;
+  tp.len_stride = Bo;
+  HIP_OR_FAIL(ctcx::launch_traceback(tp, s));
+  if (prof) HIP_OR_FAIL(hipEventRecord(v.ev[3], s));
   return CTCEXT_OK;
 }
 
 template <typename T>
-static int run_decode(ctcext_decoder* d, const ctcext_decode_args* a, const T* x, const int32_t* sl,
-                      hipStream_t s) {
+static int run_decode(ctcext_decoder* d, const ctcext_decode_args* a, const std::vector<int32_t>& hsl,
+                      hipStream_t root_stream) {
   const int64_t T_ = a->max_time, B = a->batch_size, C = a->num_classes;
-  const int W = a->beam_width, P = a->top_paths;
-  const bool prof = (a->flags & CTCEXT_FLAG_PROFILE) != 0;
-  HIP_OR_FAIL(d->norm.ensure(sizeof(T) * (size_t)(T_ * B)));
-  HIP_OR_FAIL(d->rec.ensure(sizeof(ctcx::Rec) * (size_t)(B * T_ * W)));
-  HIP_OR_FAIL(d->item.ensure(sizeof(ctcx::ItemOut) * (size_t)B));
-  HIP_OR_FAIL(d->top_pos.ensure(4 * (size_t)(B * P)));
-  HIP_OR_FAIL(d->top_kind.ensure(4 * (size_t)(B * P)));
-  HIP_OR_FAIL(d->logp.ensure(sizeof(T) * (size_t)(B * P)));
-  HIP_OR_FAIL(d->seq.ensure(4 * (size_t)(B * P * 2 * T_)));
-  HIP_OR_FAIL(d->len.ensure(4 * (size_t)(B * P * 2)));
-  HIP_OR_FAIL(d->off.ensure(8 * (size_t)(B * P * 2)));
-  HIP_OR_FAIL(d->res.ensure(8 * (size_t)(P * 4)));
+  const int P = a->top_paths;
+  const int ts = (int)sizeof(T);
+  const int nd = (int)d->devs.size();
+  Dev& root = d->devs[0];
+  std::vector<int64_t> lo;
+  shard_bounds(hsl, nd, lo);
+
+  // 1. inputs to every device, then norm + decode + traceback, all async
+  for (int i = 0; i < nd; ++i) {
+    Dev& v = d->devs[(size_t)i];
+    v.lo = lo[(size_t)i];
+    v.nb = lo[(size_t)i + 1] - lo[(size_t)i];
+    v.s = (i == 0) ? root_stream : v.own_stream;
+    if (v.nb == 0 && i > 0) continue;
+    HIP_OR_FAIL(hipSetDevice(v.device));
+    const T* x;
+    const int32_t* sl;
+    int64_t xstride;
+    if (i == 0 && a->inputs_on_device) {   // the root's shard is read in place
+      x = (const T*)a->inputs;
+      xstride = B;
+      sl = a->sequence_length;
+    } else {
+      const size_t row = (size_t)v.nb * (size_t)C * ts;
+      HIP_OR_FAIL(v.x.ensure(row * (size_t)T_ + 16));
+      HIP_OR_FAIL(v.sl.ensure(4 * (size_t)v.nb + 16));
+      const char* src = (const char*)a->inputs + (size_t)v.lo * (size_t)C * ts;
+      if (v.nb == B) {
+        HIP_OR_FAIL(hipMemcpyAsync(v.x.p, src, row * (size_t)T_, hipMemcpyDefault, v.s));
+      } else {
+        // a [T][nb][C] window of the [T][B][C] tensor: T rows of nb*C values
+        HIP_OR_FAIL(hipMemcpy2DAsync(v.x.p, row, src, (size_t)B * (size_t)C * ts, row, (size_t)T_,
+                                     hipMemcpyDefault, v.s));
+      }
+      HIP_OR_FAIL(hipMemcpyAsync(v.sl.p, hsl.data() + v.lo, 4 * (size_t)v.nb, hipMemcpyHostToDevice, v.s));
+      x = (const T*)v.x.p;
+      xstride = v.nb;
+      sl = (const int32_t*)v.sl.p;
+    }
+    int rc = enqueue_shard<T>(d, v, i == 0, a, x, xstride, sl);
+    if (rc != CTCEXT_OK) return rc;
+  }
+
+  // 2. wait for every shard; gather the per-item results to the root
   HIP_OR_FAIL(d->h_item.ensure(sizeof(ctcx::ItemOut) * (size_t)B + 16));
   HIP_OR_FAIL(d->h_res.ensure(8 * (size_t)(P * 4) + 16));
-
-  if (prof) HIP_OR_FAIL(hipEventRecord(d->ev[0], s));
-  HIP_OR_FAIL(ctcx::launch_row_norm<T>(x, sl, (T*)d->norm.p, T_, B, C, s));
-  if (prof) HIP_OR_FAIL(hipEventRecord(d->ev[1], s));
-
-  ctcx::DecodeParams<T> p{};
-  p.x = x;
-  p.norm = (const T*)d->norm.p;
-  p.seq_len = sl;
-  p.Tmax = T_; p.B = B; p.C = C;
-  p.W = W; p.P = P; p.blank = a->blank_index; p.blank_label = a->blank_label;
-  p.force_literal = (a->flags & CTCEXT_FLAG_FORCE_LITERAL) ? 1 : 0;
-  p.rec = (ctcx::Rec*)d->rec.p;
-  p.item = (ctcx::ItemOut*)d->item.p;
-  p.top_pos = (int32_t*)d->top_pos.p;
-  p.top_kind = (int32_t*)d->top_kind.p;
-  p.log_prob = (T*)d->logp.p;
-  p.prof = nullptr;
-  if (a->flags & CTCEXT_FLAG_PHASES) {
-    HIP_OR_FAIL(d->phase.ensure(8 * ctcx::kPhaseN * (size_t)B));
-    p.prof = (uint64_t*)d->phase.p;
+  for (int i = nd - 1; i >= 0; --i) {
+    Dev& v = d->devs[(size_t)i];
+    if (v.nb == 0 && i > 0) continue;
+    HIP_OR_FAIL(hipSetDevice(v.device));
+    HIP_OR_FAIL(hipStreamSynchronize(v.s));
   }
-  HIP_OR_FAIL(ctcx::launch_decode<T>(p, s));
-  if (prof) HIP_OR_FAIL(hipEventRecord(d->ev[2], s));
-
-  ctcx::TraceParams tp{};
-  tp.rec = p.rec; tp.item = p.item; tp.seq_len = sl; tp.top_pos = p.top_pos; tp.top_kind = p.top_kind;
-  tp.Tmax = T_; tp.B = B; tp.W = W; tp.P = P; tp.merge = a->merge_repeated ? 1 : 0;
-  tp.blank_label = a->blank_label;
-  tp.seq = (int32_t*)d->seq.p;
-  tp.len = (int32_t*)d->len.p;
-  HIP_OR_FAIL(ctcx::launch_traceback(tp, s));
-  HIP_OR_FAIL(ctcx::launch_scan(tp.len, (int64_t*)d->off.p, (int64_t*)d->res.p, B, P, s));
-  if (prof) HIP_OR_FAIL(hipEventRecord(d->ev[3], s));
-
-  HIP_OR_FAIL(hipMemcpyAsync(d->h_item.p, d->item.p, sizeof(ctcx::ItemOut) * (size_t)B, hipMemcpyDeviceToHost, s));
+  HIP_OR_FAIL(hipSetDevice(root.device));
+  hipStream_t s = root.s;
+  for (int i = 1; i < nd; ++i) {   // peer copies (xGMI) into the root's whole-batch buffers
+    Dev& v = d->devs[(size_t)i];
+    if (v.nb == 0) continue;
+    const size_t per = (size_t)P * 2 * (size_t)T_ * 4;
+    HIP_OR_FAIL(hipMemcpyAsync((char*)root.seq.p + (size_t)v.lo * per, v.seq.p, (size_t)v.nb * per,
+                               hipMemcpyDefault, s));
+    for (int k = 0; k < 2 * P; ++k)
+      HIP_OR_FAIL(hipMemcpyAsync((int32_t*)root.len.p + (size_t)k * B + v.lo, (int32_t*)v.len.p + (size_t)k * v.nb,
+                                 4 * (size_t)v.nb, hipMemcpyDefault, s));
+    HIP_OR_FAIL(hipMemcpyAsync((int32_t*)root.top_kind.p + (size_t)v.lo * P, v.top_kind.p, 4 * (size_t)(v.nb * P),
+                               hipMemcpyDefault, s));
+    HIP_OR_FAIL(hipMemcpyAsync((char*)root.logp.p + (size_t)(v.lo * P) * ts, v.logp.p, (size_t)(v.nb * P) * ts,
+                               hipMemcpyDefault, s));
+    HIP_OR_FAIL(hipMemcpyAsync((ctcx::ItemOut*)root.item.p + v.lo, v.item.p, sizeof(ctcx::ItemOut) * (size_t)v.nb,
+                               hipMemcpyDefault, s));
+  }
+  // 3. SparseTensor sizes over the whole batch
+  HIP_OR_FAIL(d->off.ensure(8 * (size_t)(B * P * 2)));
+  HIP_OR_FAIL(d->res.ensure(8 * (size_t)(P * 4)));
+  HIP_OR_FAIL(d->h_kind.ensure(4 * (size_t)(B * P) + 16));
+  HIP_OR_FAIL(ctcx::launch_scan((const int32_t*)root.len.p, (int64_t*)d->off.p, (int64_t*)d->res.p, B, P, s));
+  HIP_OR_FAIL(hipMemcpyAsync(d->h_item.p, root.item.p, sizeof(ctcx::ItemOut) * (size_t)B, hipMemcpyDeviceToHost, s));
   HIP_OR_FAIL(hipMemcpyAsync(d->h_res.p, d->res.p, 8 * (size_t)(P * 4), hipMemcpyDeviceToHost, s));
+  HIP_OR_FAIL(hipMemcpyAsync(d->h_kind.p, root.top_kind.p, 4 * (size_t)(B * P), hipMemcpyDeviceToHost, s));
   HIP_OR_FAIL(hipStreamSynchronize(s));
 
   d->stats = ctcext_stats{};
-  if (prof) {
-    float ms = 0;
-    (void)hipEventElapsedTime(&ms, d->ev[0], d->ev[1]); d->stats.norm_kernel_ms = ms;
-    (void)hipEventElapsedTime(&ms, d->ev[1], d->ev[2]); d->stats.decode_kernel_ms = ms;
-    (void)hipEventElapsedTime(&ms, d->ev[2], d->ev[3]); d->stats.traceback_ms = ms;
+  if (a->flags & CTCEXT_FLAG_PROFILE) {
+    for (int i = 0; i < nd; ++i) {
+      Dev& v = d->devs[(size_t)i];
+      if (v.nb == 0) continue;
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, v.ev[0], v.ev[1]);
+      d->stats.norm_kernel_ms = std::max(d->stats.norm_kernel_ms, (double)ms);
+      (void)hipEventElapsedTime(&ms, v.ev[1], v.ev[2]);
+      d->stats.decode_kernel_ms = std::max(d->stats.decode_kernel_ms, (double)ms);
+      (void)hipEventElapsedTime(&ms, v.ev[2], v.ev[3]);
+      d->stats.traceback_ms = std::max(d->stats.traceback_ms, (double)ms);
+    }
   }
   const ctcx::ItemOut* io = (const ctcx::ItemOut*)d->h_item.p;
   for (int64_t b = 0; b < B; ++b) {
-    if (io[b].error)
-      return fail(CTCEXT_INTERNAL,
-                  "beam reached a state holding the same entry twice (only reachable with -inf "
-                  "totals); not supported on the device path");
     d->stats.literal_frames += io[b].literal_steps;
     d->stats.literal_nonfinite += io[b].why_nonfinite;
-    d->stats.literal_evict_tie += io[b].why_evict_tie;
-    d->stats.literal_order_tie += io[b].why_order_tie;
+    d->stats.literal_fill += io[b].why_fill;
+    d->stats.duplicate_frames += io[b].dup_frames;
   }
   // TopPaths (decoder.h:240-243) fails on the first item with too few leaves
   for (int64_t b = 0; b < B; ++b)
     if (io[b].n_leaves < P) return fail(CTCEXT_INVALID_ARGUMENT, "Less leaves in the beam search than requested.");
+  const int32_t* kinds = (const int32_t*)d->h_kind.p;
+  for (int64_t q = 0; q < B * P; ++q) d->stats.no_label_paths += (kinds[q] < 0) ? 1 : 0;
+  (void)C;
   return CTCEXT_OK;
 }
 
-extern "C" int ctcext_decode(ctcext_decoder* d, const ctcext_decode_args* a, ctcext_path_sizes* sizes) {
+extern "C" int ctcext_decode_sharded(ctcext_decoder* d, const ctcext_decode_args* a, ctcext_path_sizes* sizes) {
   if (!d || !a) return fail(CTCEXT_INVALID_ARGUMENT, "null argument");
   d->have = false;
-  HIP_OR_FAIL(hipSetDevice(d->device));
-  if (a->dtype != CTCEXT_F32 && a->dtype != CTCEXT_F64)
-    return fail(CTCEXT_INVALID_ARGUMENT, "dtype must be float32 or float64");
-  if (a->beam_width < 1) return fail(CTCEXT_INVALID_ARGUMENT, "Value for attr 'beam_width' must be >= 1");
-  if (a->top_paths < 1) return fail(CTCEXT_INVALID_ARGUMENT, "Value for attr 'top_paths' must be >= 1");
-  const int64_t T_ = a->max_time, B = a->batch_size, C = a->num_classes;
-  if (T_ < 0 || B < 0 || C < 0) return fail(CTCEXT_INVALID_ARGUMENT, "inputs is not a 3-Tensor");
-  // kernels.cc:118-120
-  if (T_ == 0) return fail(CTCEXT_INVALID_ARGUMENT, "max_time is 0");
-  hipStream_t s = a->stream ? (hipStream_t)a->stream : d->own_stream;
-  const int ts = a->dtype == CTCEXT_F64 ? 8 : 4;
-  (void)ts;
+  int rc = validate_shapes(a);
+  if (rc != CTCEXT_OK) return rc;
+  DeviceGuard guard;
+  Dev& root = d->devs[0];
+  HIP_OR_FAIL(hipSetDevice(root.device));
+  const int64_t T_ = a->max_time, B = a->batch_size;
+  hipStream_t s = a->stream ? (hipStream_t)a->stream : root.own_stream;
 
-  // sequence_length must be read on the host for validation (kernels.cc:134-139)
+  // sequence_length is read on the host for validation (kernels.cc:134-139)
+  // and for the shard split
   std::vector<int32_t> hsl((size_t)B);
   if (B > 0) {
     if (a->inputs_on_device) {
@@ -271,40 +510,16 @@ extern "C" int ctcext_decode(ctcext_decoder* d, const ctcext_decode_args* a, ctc
       memcpy(hsl.data(), a->sequence_length, 4 * (size_t)B);
     }
   }
-  for (int64_t b = 0; b < B; ++b)
-    if (!(hsl[b] <= T_))
-      return fail(CTCEXT_FAILED_PRECONDITION,
-                  "sequence_length(" + std::to_string(b) + ") <= " + std::to_string(T_));
-  if (B > 0 && (a->blank_index < 0 || a->blank_index >= C))
-    return fail(CTCEXT_INVALID_ARGUMENT, "blank_index out of range [0, num_classes)");
-  // decoder.h:237-239 — raised by the first item's TopPaths
-  if (B > 0 && a->top_paths > a->beam_width)
-    return fail(CTCEXT_INVALID_ARGUMENT, "requested more paths than the beam width.");
-  if (B > 0 && C > ctcx::kMaxRecClasses)
-    return fail(CTCEXT_UNIMPLEMENTED, "num_classes " + std::to_string(C) + " exceeds the back-pointer record format (max " +
-                                          std::to_string(ctcx::kMaxRecClasses) + ")");
-  if (B > 0 && a->beam_width > ctcext_max_beam_width(C, a->dtype))
-    return fail(CTCEXT_UNIMPLEMENTED, "beam_width " + std::to_string(a->beam_width) + " with num_classes " +
-                                          std::to_string(C) + " exceeds the LDS-resident beam state (max " +
-                                          std::to_string(ctcext_max_beam_width(C, a->dtype)) + ")");
-
-  const void* x = a->inputs;
-  const int32_t* sl = a->sequence_length;
-  if (!a->inputs_on_device && B > 0) {
-    const size_t xb = (size_t)(T_ * B * C) * ts;
-    HIP_OR_FAIL(d->x.ensure(xb));
-    HIP_OR_FAIL(d->sl.ensure(4 * (size_t)B));
-    HIP_OR_FAIL(hipMemcpyAsync(d->x.p, a->inputs, xb, hipMemcpyHostToDevice, s));
-    HIP_OR_FAIL(hipMemcpyAsync(d->sl.p, hsl.data(), 4 * (size_t)B, hipMemcpyHostToDevice, s));
-    x = d->x.p;
-    sl = (const int32_t*)d->sl.p;
-  }
+  rc = check_lengths(hsl.data(), B, T_);
+  if (rc == CTCEXT_OK) rc = check_limits(a);
+  if (rc != CTCEXT_OK) return rc;
 
   const int P = a->top_paths;
+  d->B = B;
   d->sizes.assign((size_t)P, ctcext_path_sizes{0, 0, 0, 0});
+  d->stats = ctcext_stats{};
   if (B > 0) {
-    int rc = (a->dtype == CTCEXT_F32) ? run_decode<float>(d, a, (const float*)x, sl, s)
-                                      : run_decode<double>(d, a, (const double*)x, sl, s);
+    rc = (a->dtype == CTCEXT_F32) ? run_decode<float>(d, a, hsl, s) : run_decode<double>(d, a, hsl, s);
     if (rc != CTCEXT_OK) return rc;
     const int64_t* r = (const int64_t*)d->h_res.p;
     for (int p = 0; p < P; ++p) {
@@ -313,27 +528,28 @@ extern "C" int ctcext_decode(ctcext_decoder* d, const ctcext_decode_args* a, ctc
       d->sizes[p].num_alignment = r[(p * 2 + 1) * 2];
       d->sizes[p].max_alignment = r[(p * 2 + 1) * 2 + 1];
     }
-    // paths whose alignment is empty although the item had frames or not:
-    // the reference prints "No label seq available" for each (host side)
-    std::vector<int32_t> kinds((size_t)(B * P));
-    HIP_OR_FAIL(hipMemcpy(kinds.data(), d->top_kind.p, 4 * (size_t)(B * P), hipMemcpyDeviceToHost));
-    for (int32_t k : kinds) d->stats.no_label_paths += (k < 0) ? 1 : 0;
   }
   d->have = true;
   d->dtype = a->dtype;
-  d->T = T_; d->B = B; d->C = C; d->W = a->beam_width; d->P = P;
-  d->stream = s;
+  d->T = T_; d->C = a->num_classes; d->W = a->beam_width; d->P = P;
+  root.s = s;
   if (sizes)
     for (int p = 0; p < P; ++p) sizes[p] = d->sizes[p];
   g_err.clear();
   return CTCEXT_OK;
 }
 
+extern "C" int ctcext_decode(ctcext_decoder* d, const ctcext_decode_args* a, ctcext_path_sizes* sizes) {
+  return ctcext_decode_sharded(d, a, sizes);
+}
+
 extern "C" int ctcext_fetch(ctcext_decoder* d, const ctcext_outputs* o) {
   if (!d || !o) return fail(CTCEXT_INVALID_ARGUMENT, "null argument");
   if (!d->have) return fail(CTCEXT_FAILED_PRECONDITION, "ctcext_fetch without a successful ctcext_decode");
-  HIP_OR_FAIL(hipSetDevice(d->device));
-  hipStream_t s = d->stream;
+  DeviceGuard guard;
+  Dev& root = d->devs[0];
+  HIP_OR_FAIL(hipSetDevice(root.device));
+  hipStream_t s = root.s;
   const int P = d->P;
   const int64_t B = d->B;
   const int ts = d->dtype == CTCEXT_F64 ? 8 : 4;
@@ -373,8 +589,8 @@ extern "C" int ctcext_fetch(ctcext_decoder* d, const ctcext_outputs* o) {
     for (int k = 0; k < P * 2; ++k) { both[k] = idx[k]; both[P * 2 + k] = val[k]; }
     HIP_OR_FAIL(hipMemcpyAsync(dp, both.data(), sizeof(int64_t*) * (size_t)P * 4, hipMemcpyHostToDevice, s));
     ctcx::PackParams pp{};
-    pp.seq = (const int32_t*)d->seq.p;
-    pp.len = (const int32_t*)d->len.p;
+    pp.seq = (const int32_t*)root.seq.p;
+    pp.len = (const int32_t*)root.len.p;
     pp.off = (const int64_t*)d->off.p;
     pp.Tmax = d->T; pp.B = B; pp.P = P;
     pp.idx = dp;
@@ -387,7 +603,7 @@ extern "C" int ctcext_fetch(ctcext_decoder* d, const ctcext_outputs* o) {
     HIP_OR_FAIL(hipMemcpyAsync(o->alignment_shape[p], &shapes[p * 4 + 2], 16, to_dev, s));
   }
   if (B > 0) {
-    HIP_OR_FAIL(hipMemcpyAsync(o->log_probability, d->logp.p, (size_t)(B * P) * ts,
+    HIP_OR_FAIL(hipMemcpyAsync(o->log_probability, root.logp.p, (size_t)(B * P) * ts,
                                o->outputs_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s));
     if (!o->outputs_on_device) {
       for (int p = 0; p < P; ++p) {

@@ -17,15 +17,17 @@
 //   ctcx_pack         int64 SparseTensor components (StoreAllDecodedSequences).
 //
 // The beam update per frame has two exact implementations:
-//   * the FAST path: slot model — beams sit at fixed LDS slots, their totals in
-//     registers; the streaming top-W is a sequence of (evict the unique minimum,
-//     insert) events found by wave ballots; final order by a rank sort.  Exact
-//     whenever no two live totals are equal at an eviction or in the final
-//     order and every total is finite (checked each frame).
-//   * the LITERAL path (one lane): the reference's own TopN state machine and
-//     libstdc++ heap/introsort layout over slot ids (ctcx_topn.h).  A frame
-//     whose fast path hits a tie or a non-finite total is replayed here from
-//     the untouched frame-start state, so tie order matches the reference.
+//   * the FAST path (exact_step, whole wave): beams sit at LDS slots; offers are
+//     scored 64 per chunk and the accepted ones are pushed, in offer order,
+//     into an LDS replica of gtl::TopN's libstdc++ heap (wave-parallel sift:
+//     one ballot finds the path, a second the stop), so evictions and the
+//     sort_heap Extract order of tied totals are the reference's.
+//   * the LITERAL path (literal_step, one lane): the reference's TopN state
+//     machine verbatim over slot ids (ctcx_topn.h), for the frames the fast
+//     path does not model: a non-finite logit or total, the beam filling up in
+//     the middle of the grow loop (TopN then peeks lazily), and a beam that
+//     holds one entry twice (reachable with -inf logits, decoder.h:142 +
+//     189-199).  Such a frame is replayed from the untouched frame-start state.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -169,6 +171,9 @@ struct Ctx {
   CTCX_LDS uint32_t* ebpb; CTCX_LDS uint32_t* ebpn; CTCX_LDS uint32_t* ekind;
   CTCX_LDS int* elab; CTCX_LDS int* eflg;
   CTCX_LDS int* heap; CTCX_LDS int* tops; CTCX_LDS int* freel; CTCX_LDS int* sorted;
+  // per branch position: the first position holding the same entry (the
+  // reference's beam can hold one BeamEntry twice, see literal_step)
+  CTCX_LDS int* alias;
   CTCX_LDS T* row;
   CTCX_LDS int* misc;
   // prefix identity: 128-bit hash of each branch's label prefix and of its
@@ -249,6 +254,7 @@ __host__ __device__ void carve(Ctx<T>& cx, CTCX_LDS char* base, int Wcap, int W,
   cx.tops = (CTCX_LDS int*)p; p += a16(((size_t)Wcap + 1) * 4);
   cx.freel = (CTCX_LDS int*)p; p += a16(ENC * 4);
   cx.sorted = (CTCX_LDS int*)p; p += a16((size_t)Wcap * 4);
+  cx.alias = (CTCX_LDS int*)p; p += a16((size_t)Wcap * 4);
   cx.misc = (CTCX_LDS int*)p; p += 64;
   for (int b = 0; b < 2; ++b) {
     CTCX_LDS uint64_t* q = (CTCX_LDS uint64_t*)p;
@@ -278,11 +284,14 @@ __host__ __device__ __forceinline__ void cand_from(const Ctx<T>& cx, int buf, in
   best.push(base + p, has ? (((uint32_t)src << 1) | (uint32_t)kind) : kBpRestart);
 }
 
-// Recursion for branch i (decoder.h:95-143).  Reads the frame-start branch
-// arrays and the entry i's current newp (rolled = oldp, except in literal mode
-// where a parent processed earlier may have changed its own entry).
+// Recursion for the branch at position i (decoder.h:95-143) into its entry e
+// (e == i, except for a second occurrence of an entry the beam holds twice,
+// whose entry is its first occurrence's).  Reads the frame-start branch arrays
+// and the entry's current newp (rolled = oldp, except in literal mode where a
+// parent processed earlier, or an earlier occurrence, may have changed it).
 template <typename T>
-__host__ __device__ __forceinline__ void recurse_branch(const Ctx<T>& cx, int buf, int i, T norm, bool literal) {
+__host__ __device__ __forceinline__ void recurse_branch(const Ctx<T>& cx, int buf, int i, int e, T norm,
+                                                        bool literal) {
   const T NI = ninf<T>();
   const int f = sel(cx.flg, buf)[i];
   const int L = sel(cx.lab, buf)[i];
@@ -291,7 +300,7 @@ __host__ __device__ __forceinline__ void recurse_branch(const Ctx<T>& cx, int bu
   const bool fresh = (o_t == NI);
   // restart base for a from-blank candidate with receiver i
   const T rs_blank = (isroot || ((f & F_PROOT) && fresh)) ? T(0) : NI;
-  T nl = cx.el[i];
+  T nl = cx.el[e];
   Best<T> bn{T(0), kBpNone, false}, bb{T(0), kBpNone, false};
   if (!isroot) {
     const T xl = cx.row[L];
@@ -313,24 +322,25 @@ __host__ __device__ __forceinline__ void recurse_branch(const Ctx<T>& cx, int bu
   const T xb = cx.row[cx.blank];
   const T nbk = o_t + xb - norm;
   const T pb = xb - norm;
-  // existing new candidates (literal replay of a duplicate visit) are kept
-  const int ef = cx.eflg[i];
-  if (ef & F_HB) { bb.ok = true; bb.p = cx.ecb[i]; bb.bp = cx.ebpb[i]; }
+  // new candidates pushed by an earlier occurrence of the same entry are kept
+  // (first-pushed maximum across both visits)
+  const int ef = cx.eflg[e];
+  if (ef & F_HB) { bb.ok = true; bb.p = cx.ecb[e]; bb.bp = cx.ebpb[e]; }
   if (ef & F_HN) {
-    Best<T> prior{cx.ecn[i], cx.ebpn[i], true};
+    Best<T> prior{cx.ecn[e], cx.ebpn[e], true};
     if (bn.ok) prior.push(bn.p, bn.bp);
     bn = prior;
   }
   cand_from(cx, buf, i, 0, pb, rs_blank, bb);
   cand_from(cx, buf, i, 1, pb, NI, bb);
-  cx.eb[i] = nbk;
-  cx.el[i] = nl;
-  cx.et[i] = lse(nbk, nl);
-  cx.ecb[i] = bb.p; cx.ebpb[i] = bb.bp;
-  cx.ecn[i] = bn.p; cx.ebpn[i] = bn.bp;
-  cx.eflg[i] = (bb.ok ? F_HB : 0) | (bn.ok ? F_HN : 0);
-  cx.ekind[i] = ((uint32_t)i << 1);
-  cx.elab[i] = L;
+  cx.eb[e] = nbk;
+  cx.el[e] = nl;
+  cx.et[e] = lse(nbk, nl);
+  cx.ecb[e] = bb.p; cx.ebpb[e] = bb.bp;
+  cx.ecn[e] = bn.p; cx.ebpn[e] = bn.bp;
+  cx.eflg[e] = (bb.ok ? F_HB : 0) | (bn.ok ? F_HN : 0);
+  cx.ekind[e] = ((uint32_t)e << 1);
+  cx.elab[e] = L;
 }
 
 // ---------------------------------------------------------------------------
@@ -716,7 +726,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     cx.bloom[i] = 0;
   }
   __syncthreads();
-  for (int i = lane; i < nb; i += 64) recurse_branch(cx, buf, i, norm, false);
+  for (int i = lane; i < nb; i += 64) recurse_branch(cx, buf, i, i, norm, false);
   __syncthreads();
   bool nonfinite = false;
   for (int i = lane; i < nb; i += 64) {
@@ -1147,25 +1157,52 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
 // LITERAL path for one frame, executed by lane 0 (decoder.h:69-210 verbatim in
 // semantics, including TopN layout).  Returns the number of surviving entries
 // (sorted slots in cx.sorted); for the last frame also fills cx.tops[0..P)
-// with the TopPaths selection as slots.  *err = 1 on a duplicate-beam state.
+// with the TopPaths selection as positions.
+//
+// Duplicate entries.  With -inf totals the reference can push one BeamEntry
+// twice: every branch is pushed after its recursion (decoder.h:142), and a
+// branch whose new total is -inf is not Active, so its parent's grow loop
+// re-creates it and pushes it again (decoder.h:168, 189-199).  Extract() then
+// hands the entry out twice and the next Step visits it twice:
+//   * the second roll copies the already reset new_cands into old_cands, so a
+//     duplicated entry starts the frame without alignment candidates
+//     (decoder.h:87-92);
+//   * the second recursion accumulates into the newp.label the first one wrote
+//     and keeps the first one's candidates (decoder.h:102-139);
+//   * its grow loop runs twice over the same children (GetChild is the same
+//     node), and deactivating or evicting the node affects every occurrence.
+// Positions holding the same entry are linked by cx.alias (the first
+// occurrence, which owns the entry slot); dup_in says this frame has any, and
+// *dup_out that the next one does.
 template <typename T>
-__host__ __device__ __attribute__((noinline)) int literal_step(Ctx<T> cx, int buf, int nb, T norm, bool last, int P, int* err,
-                            int* n_leaves) {
+__host__ __device__ __attribute__((noinline)) int literal_step(Ctx<T> cx, int buf, int nb, T norm, bool last, int P,
+                                                               bool dup_in, int* dup_out, int* n_leaves) {
   const T NI = ninf<T>();
   const int W = cx.W, C = cx.C, blank = cx.blank;
+  // roll (decoder.h:87-92)
   for (int i = 0; i < nb; ++i) {
-    cx.et[i] = sel(cx.ot, buf)[i]; cx.eb[i] = sel(cx.ob, buf)[i]; cx.el[i] = sel(cx.ol, buf)[i];
-    cx.eflg[i] = 0;
-    cx.bst[i] = 0;
+    const int a = dup_in ? cx.alias[i] : i;
+    if (a == i) {
+      cx.et[i] = sel(cx.ot, buf)[i]; cx.eb[i] = sel(cx.ob, buf)[i]; cx.el[i] = sel(cx.ol, buf)[i];
+      cx.eflg[i] = 0;
+      cx.bst[i] = 0;
+    } else {   // a second roll of the entry: old_cands = (reset) new_cands
+      sel(cx.flg, buf)[i] &= ~(F_HB | F_HN);
+      sel(cx.flg, buf)[a] &= ~(F_HB | F_HN);
+    }
   }
   int nfree = 0;
-  for (int s = cx.enc - 1; s >= nb; --s) cx.freel[nfree++] = s;
+  for (int s = cx.enc - 1; s >= nb; --s) {
+    cx.freel[nfree++] = s;
+    if (dup_in) cx.ekind[s] = 0xFFFFFFFFu;   // no stale match in the child lookup below
+  }
   SlotGreater<T> gt{cx.et};
   LitTop h{cx.heap, 0, W, kTopUnordered};
 
   for (int i = 0; i < nb; ++i) {
-    recurse_branch(cx, buf, i, norm, true);
-    lit_top_push(h, i, gt);
+    const int a = dup_in ? cx.alias[i] : i;
+    recurse_branch(cx, buf, i, a, norm, true);
+    lit_top_push(h, a, gt);
   }
 
   for (int i = 0; i < nb; ++i) {
@@ -1173,13 +1210,22 @@ __host__ __device__ __attribute__((noinline)) int literal_step(Ctx<T> cx, int bu
       const T bt = sel(cx.ot, buf)[i];
       if (!(bt > NI && (h.size() < W || bt > cx.et[lit_top_peek_bottom(h, gt)]))) continue;
     }
+    const int a = dup_in ? cx.alias[i] : i;
     const int bl = sel(cx.lab, buf)[i];
     const int bflg = sel(cx.flg, buf)[i];
     for (int l = 0; l < C; ++l) {
       if (l == blank) continue;
       int c = -1;
-      for (int k = cx.head[i]; k >= 0; k = cx.sib[k])
+      for (int k = cx.head[a]; k >= 0; k = cx.sib[k])
         if (sel(cx.lab, buf)[k] == l) { c = k; break; }
+      if (c < 0 && dup_in) {
+        // GetChild of an entry visited twice: the child an earlier visit created
+        // this frame is the same node (Active: skipped; otherwise re-created)
+        bool act = false;
+        for (int s = nb; s < cx.enc; ++s)
+          if (cx.ekind[s] == (((uint32_t)a << 1) | 1u) && cx.elab[s] == l && cx.et[s] != NI) { act = true; break; }
+        if (act) continue;
+      }
       int slot;
       const bool fresh_slot = (c < 0);
       if (!fresh_slot) {
@@ -1202,7 +1248,7 @@ __host__ __device__ __attribute__((noinline)) int literal_step(Ctx<T> cx, int bu
       cx.ecn[slot] = cd.p; cx.ebpn[slot] = cd.bp;
       cx.eflg[slot] |= F_HN;
       cx.et[slot] = cx.el[slot];
-      cx.ekind[slot] = fresh_slot ? (((uint32_t)i << 1) | 1u) : ((uint32_t)c << 1);
+      cx.ekind[slot] = fresh_slot ? (((uint32_t)a << 1) | 1u) : ((uint32_t)c << 1);
       cx.elab[slot] = l;
       const T ct = cx.et[slot];
       if (ct > NI && (h.size() < W || ct > cx.et[lit_top_peek_bottom(h, gt)])) {
@@ -1215,11 +1261,17 @@ __host__ __device__ __attribute__((noinline)) int literal_step(Ctx<T> cx, int bu
         }
         lit_top_push(h, slot, gt);
       } else {
+        // deactivate the child (decoder.h:200-205); a branch child's oldp and
+        // old_cands are its frame-start arrays, at every position holding it
         cx.et[slot] = NI; cx.eb[slot] = NI; cx.el[slot] = NI;
         cx.eflg[slot] = 0;
         if (!fresh_slot) {
-          sel(cx.ot, buf)[c] = NI; sel(cx.ob, buf)[c] = NI; sel(cx.ol, buf)[c] = NI;
-          sel(cx.flg, buf)[c] &= ~(F_HB | F_HN);
+          for (int j = c; j < nb; ++j) {
+            if (j != c && !(dup_in && cx.alias[j] == c)) continue;
+            sel(cx.ot, buf)[j] = NI; sel(cx.ob, buf)[j] = NI; sel(cx.ol, buf)[j] = NI;
+            sel(cx.flg, buf)[j] &= ~(F_HB | F_HN);
+            if (!dup_in) break;
+          }
         }
       }
     }
@@ -1233,14 +1285,18 @@ __host__ __device__ __attribute__((noinline)) int literal_step(Ctx<T> cx, int bu
     lit_top_extract(tp, gt);
   }
   const int n = lit_top_extract(h, gt);
-  // slot -> sorted position (freel reused as the map; -1 = not a leaf)
+  // slot -> first sorted position (freel reused as the map; -1 = not a leaf);
+  // the next frame's aliases
   for (int s = 0; s < cx.enc; ++s) cx.freel[s] = -1;
+  int dup = 0;
   for (int k = 0; k < n; ++k) {
     const int s = cx.heap[k];
-    if (cx.freel[s] >= 0) *err = 1;     // the same entry twice in the beam
-    cx.freel[s] = k;
+    if (cx.freel[s] < 0) cx.freel[s] = k;
+    else dup = 1;
     cx.sorted[k] = s;
+    cx.alias[k] = cx.freel[s];
   }
+  *dup_out = dup;
   if (last) {
     const int lim = (P < *n_leaves) ? P : *n_leaves;
     for (int q = 0; q < lim; ++q) cx.tops[q] = cx.freel[cx.tops[q]];
@@ -1271,11 +1327,12 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     cx.cb[0][0] = T(0); cx.cn[0][0] = T(0);
     cx.ha[0][0] = kRootHa; cx.hb[0][0] = kRootHb; cx.pha[0][0] = 0; cx.phb[0][0] = 0;
     cx.head[0] = -1;
+    cx.alias[0] = 0;
   }
   int nb = 1;
   int literal_steps = 0;
-  int why_nf = 0, why_et = 0, why_ot = 0;
-  int err = 0;
+  int why_nf = 0, why_fill = 0, dup_frames = 0;
+  bool dup = false;   // this frame's beam holds an entry twice (literal frames only)
   int n_leaves = 1;
   __syncthreads();
 
@@ -1290,7 +1347,7 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
 #endif
   for (int t = 0; t < sl; ++t) {
     uint64_t t0 = prof ? __builtin_amdgcn_s_memtime() : 0;
-    const T* xr = prm.x + ((int64_t)t * B + b) * C;
+    const T* xr = prm.x + ((int64_t)t * prm.xstride + b) * C;
     for (int j = lane; j < C; j += 64) cx.row[j] = xr[j];
     const T norm = prm.norm[(int64_t)t * B + b];
     __syncthreads();
@@ -1301,21 +1358,24 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     int nl_fast = 0;
     uint64_t t1 = prof ? __builtin_amdgcn_s_memtime() : 0;
     if (prof) pc[0] += t1 - t0;
-    if (!prm.force_literal) why = exact_step<T, RN, BIG>(cx, buf, nb, norm, last, prm.P, &n, &nl_fast, prof ? pc : nullptr);
+    if (!prm.force_literal && !dup)
+      why = exact_step<T, RN, BIG>(cx, buf, nb, norm, last, prm.P, &n, &nl_fast, prof ? pc : nullptr);
     __syncthreads();
     uint64_t t2 = prof ? __builtin_amdgcn_s_memtime() : 0;
     const bool ok = (why == 0);
-    why_nf += (why == 1); why_et += (why == 2);
+    why_nf += (why == 1); why_fill += (why == 2);
+    dup_frames += dup ? 1 : 0;
+    bool dup_next = false;
     if (!ok) {
       if (lane == 0) {
-        int e2 = 0, nl = 0;
-        misc[0] = literal_step(cx, buf, nb, norm, last, prm.P, &e2, &nl);
-        misc[1] = e2;
+        int d2 = 0, nl = 0;
+        misc[0] = literal_step(cx, buf, nb, norm, last, prm.P, dup, &d2, &nl);
+        misc[1] = d2;
         misc[2] = nl;
       }
       __syncthreads();
       n = misc[0];
-      err |= misc[1];
+      dup_next = misc[1] != 0;
       n_leaves = misc[2];
       ++literal_steps;
     } else {
@@ -1329,8 +1389,12 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     const int nx = buf ^ 1;
     for (int i = lane; i < nb; i += 64) cx.newpos[i] = -1;
     __syncthreads();
+    // (an entry the beam holds twice: its first position is the canonical one,
+    // the one its children link to and the hash table maps to)
     for (int k = lane; k < n; k += 64) {
       const uint32_t kd = cx.ekind[cx.sorted[k]];
+      if (!dup_next) cx.alias[k] = k;
+      else if (cx.alias[k] != k) continue;
       if (!(kd & 1u)) cx.newpos[kd >> 1] = k;
     }
     for (int q = lane; q < cx.hts; q += 64) cx.htab[q] = -1;
@@ -1345,7 +1409,8 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
         hmix(pa, pb, cx.elab[cx.sorted[k]], ha, hb);
         int q = (int)(ha & (uint64_t)(cx.hts - 1));
         int expect = -1;
-        while (!__hip_atomic_compare_exchange_strong(&cx.htab[q], &expect, k, __ATOMIC_RELAXED,
+        while ((!dup_next || cx.alias[k] == k) &&
+               !__hip_atomic_compare_exchange_strong(&cx.htab[q], &expect, k, __ATOMIC_RELAXED,
                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
           q = (q + 1) & (cx.hts - 1);
           expect = -1;
@@ -1395,11 +1460,12 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     __syncthreads();
     buf = nx;
     nb = n;
+    dup = dup_next;
     for (int k = lane; k < nb; k += 64) cx.head[k] = -1;
     __syncthreads();
     for (int k = lane; k < nb; k += 64) {
       const int pp = sel(cx.par, buf)[k];
-      if (pp >= 0)
+      if (pp >= 0 && (!dup || cx.alias[k] == k))
         cx.sib[k] = __hip_atomic_exchange(&cx.head[pp], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     __syncthreads();
@@ -1432,11 +1498,10 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     ItemOut io;
     io.n_leaves = n_leaves;
     io.literal_steps = literal_steps;
-    io.error = err;
+    io.dup_frames = dup_frames;
     io.why_nonfinite = why_nf;
-    io.why_evict_tie = why_et;
-    io.why_order_tie = why_ot;
-    io.pad[0] = io.pad[1] = 0;
+    io.why_fill = why_fill;
+    io.pad[0] = io.pad[1] = io.pad[2] = 0;
     prm.item[b] = io;
   }
 }
@@ -1454,12 +1519,13 @@ __host__ __device__ __forceinline__ double norm_log(double x) { return gm::log(x
 
 template <typename T>
 __global__ __launch_bounds__(256) void ctcx_row_norm(const T* __restrict__ x, const int32_t* seq_len,
-                                                    T* __restrict__ norm, int64_t Tmax, int64_t B, int64_t C) {
+                                                    T* __restrict__ norm, int64_t Tmax, int64_t B, int64_t C,
+                                                    int64_t xstride) {
   const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (row >= Tmax * B) return;
   const int64_t t = row / B, b = row - t * B;
   if (t >= seq_len[b]) return;
-  const T* r = x + row * C;
+  const T* r = x + (t * xstride + b) * C;
   T m = r[0];
   for (int64_t j = 1; j < C; ++j) m = (r[j] > m) ? r[j] : m;
   T s = T(0);
@@ -1509,7 +1575,7 @@ __global__ __launch_bounds__(256) void ctcx_traceback(TraceParams tp) {
       }
     }
   }
-  tp.len[((int64_t)p * 2 + which) * tp.B + b] = len;
+  tp.len[((int64_t)p * 2 + which) * tp.len_stride + b] = len;
 }
 
 // Exclusive scan of lengths per (path, kind); also totals and maxima.
@@ -1604,15 +1670,18 @@ template hipError_t launch_decode<float>(const DecodeParams<float>&, hipStream_t
 template hipError_t launch_decode<double>(const DecodeParams<double>&, hipStream_t);
 
 template <typename T>
-hipError_t launch_row_norm(const T* x, const int32_t* sl, T* norm, int64_t T_, int64_t B, int64_t C, hipStream_t s) {
+hipError_t launch_row_norm(const T* x, const int32_t* sl, T* norm, int64_t T_, int64_t B, int64_t C,
+                           int64_t xstride, hipStream_t s) {
   const int64_t rows = T_ * B;
   if (rows == 0) return hipSuccess;
-  hipLaunchKernelGGL(ctcx_row_norm<T>, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, x, sl, norm, T_, B, C);
+  hipLaunchKernelGGL(ctcx_row_norm<T>, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, x, sl, norm, T_, B, C,
+                     xstride);
   return hipGetLastError();
 }
-template hipError_t launch_row_norm<float>(const float*, const int32_t*, float*, int64_t, int64_t, int64_t, hipStream_t);
+template hipError_t launch_row_norm<float>(const float*, const int32_t*, float*, int64_t, int64_t, int64_t, int64_t,
+                                           hipStream_t);
 template hipError_t launch_row_norm<double>(const double*, const int32_t*, double*, int64_t, int64_t, int64_t,
-                                            hipStream_t);
+                                            int64_t, hipStream_t);
 
 hipError_t launch_traceback(const TraceParams& tp, hipStream_t s) {
   const int64_t n = tp.B * tp.P * 2;

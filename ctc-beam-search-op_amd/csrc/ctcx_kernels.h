@@ -52,19 +52,19 @@ constexpr int kMaxRecClasses = 65535;
 struct ItemOut {
   int32_t n_leaves;       // leaves_.size() after the last frame
   int32_t literal_steps;  // frames replayed through the literal TopN model
-  int32_t error;          // 0 ok, 1 = unsupported duplicate-beam state
-  int32_t why_nonfinite;  // literal replays caused by a non-finite total
-  int32_t why_evict_tie;  // ... by equal totals at an eviction
-  int32_t why_order_tie;  // ... by equal totals in the final order
-  int32_t pad[2];
+  int32_t dup_frames;     // frames whose beam held one entry twice (-inf logits)
+  int32_t why_nonfinite;  // literal replays caused by a non-finite logit or total
+  int32_t why_fill;       // ... by the beam filling up mid-frame
+  int32_t pad[3];
 };
 
 template <typename T>
 struct DecodeParams {
-  const T* x;               // [Tmax][B][C]
+  const T* x;               // row (t, b) at x + (t * xstride + b) * C
   const T* norm;            // [Tmax][B]  softmax normaliser per row
   const int32_t* seq_len;   // [B]
   int64_t Tmax, B, C;
+  int64_t xstride;          // items per frame in x (B, or the full batch for a shard read in place)
   int32_t W, P, blank, blank_label;
   int32_t force_literal;    // testing knob: replay every frame literally
   Rec* rec;                 // [B][Tmax][W]
@@ -84,7 +84,8 @@ struct TraceParams {
   int64_t Tmax, B;
   int32_t W, P, merge, blank_label;
   int32_t* seq;    // [B][P][2][Tmax]  walk output, reversed
-  int32_t* len;    // [P][2][B]
+  int32_t* len;    // [P][2][len_stride], this batch's items at [.][.][0, B)
+  int64_t len_stride;
 };
 
 struct PackParams {
@@ -121,6 +122,7 @@ __host__ __device__ inline size_t decode_lds_bytes(int W, int64_t C, int tsize) 
   s += a16(((size_t)W + 1) * 4) * 2;            // heap, top-paths scratch
   s += a16(ENC * 4);                            // free list / slot map
   s += a16((size_t)W * 4);                      // sorted
+  s += a16((size_t)W * 4);                      // alias (entries the beam holds twice)
   s += 64;                                      // scalars
   s += 2 * 4 * (size_t)W * 8;                   // prefix hashes, 2 buffers
   s += a16(4 * (size_t)htab_size(W));           // per-frame new-leaf hash table

@@ -24,9 +24,9 @@ CTCEXT_FLAG_PROFILE = 2
 CTCEXT_FLAG_PHASES = 4
 
 # every symbol include/ctcext.h declares
-EXPORTED_SYMBOLS = ("ctcext_create", "ctcext_destroy", "ctcext_decode", "ctcext_fetch",
-                    "ctcext_get_stats", "ctcext_last_error", "ctcext_max_beam_width",
-                    "ctcext_phase_counters")
+EXPORTED_SYMBOLS = ("ctcext_create", "ctcext_create_sharded", "ctcext_destroy", "ctcext_validate",
+                    "ctcext_decode", "ctcext_decode_sharded", "ctcext_fetch", "ctcext_get_stats",
+                    "ctcext_last_error", "ctcext_max_beam_width", "ctcext_phase_counters")
 
 
 class DecodeArgs(ctypes.Structure):
@@ -37,7 +37,9 @@ class DecodeArgs(ctypes.Structure):
                 ("beam_width", ctypes.c_int32), ("top_paths", ctypes.c_int32),
                 ("merge_repeated", ctypes.c_int32), ("blank_index", ctypes.c_int32),
                 ("blank_label", ctypes.c_int32), ("flags", ctypes.c_int32),
-                ("stream", ctypes.c_void_p)]
+                ("stream", ctypes.c_void_p),
+                ("inputs_dims", ctypes.c_int32), ("sequence_length_dims", ctypes.c_int32),
+                ("sequence_length_size", ctypes.c_int64)]
 
 
 class PathSizes(ctypes.Structure):
@@ -58,10 +60,11 @@ class Outputs(ctypes.Structure):
 
 class Stats(ctypes.Structure):
     _fields_ = [("literal_frames", ctypes.c_int64), ("literal_nonfinite", ctypes.c_int64),
-                ("literal_evict_tie", ctypes.c_int64), ("literal_order_tie", ctypes.c_int64),
+                ("literal_fill", ctypes.c_int64), ("duplicate_frames", ctypes.c_int64),
                 ("no_label_paths", ctypes.c_int64),
                 ("decode_kernel_ms", ctypes.c_double), ("norm_kernel_ms", ctypes.c_double),
-                ("traceback_ms", ctypes.c_double)]
+                ("traceback_ms", ctypes.c_double), ("n_devices", ctypes.c_int32),
+                ("pad_", ctypes.c_int32)]
 
 
 _lib = None
@@ -86,6 +89,12 @@ def load():
     lib = ctypes.CDLL(LIB_PATH)
     lib.ctcext_create.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
     lib.ctcext_create.restype = ctypes.c_int
+    lib.ctcext_create_sharded.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+    lib.ctcext_create_sharded.restype = ctypes.c_int
+    lib.ctcext_validate.argtypes = [ctypes.POINTER(DecodeArgs)]
+    lib.ctcext_validate.restype = ctypes.c_int
+    lib.ctcext_decode_sharded.argtypes = [ctypes.c_void_p, ctypes.POINTER(DecodeArgs), ctypes.POINTER(PathSizes)]
+    lib.ctcext_decode_sharded.restype = ctypes.c_int
     lib.ctcext_destroy.argtypes = [ctypes.c_void_p]
     lib.ctcext_destroy.restype = None
     lib.ctcext_decode.argtypes = [ctypes.c_void_p, ctypes.POINTER(DecodeArgs), ctypes.POINTER(PathSizes)]

@@ -12,7 +12,16 @@ components to the root, over RCCL (backend "nccl") on MI355X / xGMI:
 
 The root shifts each rank's batch indices by the rank's first item and
 concatenates in rank order, which is exactly the single-device output order
-for contiguous shards.  Works with gloo on CPU tensors (tests).
+for contiguous shards.
+
+The collective is chosen per backend, up front (no exception-driven retry: a
+collective that fails on some ranks only would leave the others inside a
+different one): RCCL ("nccl") gathers the device tensors directly; gloo runs
+its collectives on host copies (its gather takes CPU tensors), which is how
+the CPU tests and a one-GPU multi-rank rehearsal run.
+
+For one process driving several GPUs, use the op's ``devices=`` argument
+instead (ctcext_create_sharded: peer-copy gather inside the library).
 """
 import torch
 import torch.distributed as dist
@@ -29,17 +38,23 @@ def shard_bounds(batch, rank, world):
     return lo, lo + per + (1 if rank < rem else 0)
 
 
+def _host_collectives(group):
+    """gloo: collectives on CPU tensors; nccl (RCCL): on the device tensors."""
+    return dist.get_backend(group) == "gloo"
+
+
 def _gather(t, dst, group, world):
-    """dist.gather where supported; all_gather otherwise (same result on dst)."""
+    """dist.gather of equal-sized tensors to ``dst`` (a list there, None elsewhere),
+    returned on ``t``'s device."""
     rank = dist.get_rank(group)
-    try:
-        lst = [torch.empty_like(t) for _ in range(world)] if rank == dst else None
-        dist.gather(t, lst, dst=dst, group=group)
-        return lst
-    except (RuntimeError, ValueError):
-        lst = [torch.empty_like(t) for _ in range(world)]
-        dist.all_gather(lst, t, group=group)
-        return lst if rank == dst else None
+    dev = t.device
+    if _host_collectives(group):
+        t = t.cpu()
+    lst = [torch.empty_like(t) for _ in range(world)] if rank == dst else None
+    dist.gather(t, lst, dst=dst, group=group)
+    if lst is None:
+        return None
+    return [x.to(dev) for x in lst]
 
 
 def gather_to_root(out, first_item, top_paths, dst=0, group=None):
@@ -53,7 +68,8 @@ def gather_to_root(out, first_item, top_paths, dst=0, group=None):
     for p in range(P):
         counts += [out.decoded_values[p].numel(), int(out.decoded_shape[p][1]),
                    out.alignment_values[p].numel(), int(out.alignment_shape[p][1])]
-    hdr = torch.tensor(counts + [first_item, out.log_probability.shape[0]], dtype=torch.int64, device=dev)
+    hdr = torch.tensor(counts + [first_item, out.log_probability.shape[0]], dtype=torch.int64,
+                       device="cpu" if _host_collectives(group) else dev)
     hdrs = [torch.empty_like(hdr) for _ in range(world)]
     dist.all_gather(hdrs, hdr, group=group)
     hdrs = [h.cpu().tolist() for h in hdrs]

@@ -46,13 +46,16 @@ enum {
 
 typedef struct ctcext_decoder ctcext_decoder;
 
-/* Replaces the op's inputs + attrs (ops.cc:10-17). */
+/* Replaces the op's inputs + attrs (ops.cc:10-17).  The two input tensors
+ * travel as (pointer, rank, sizes), the way an OpKernel sees them, so that the
+ * reference's shape checks (kernels.cc:111-131) run behind this ABI. */
 typedef struct {
   int32_t dtype;                   /* CTCEXT_F32 / CTCEXT_F64 */
-  int32_t inputs_on_device;        /* 1: inputs/sequence_length are device (HBM) pointers */
+  int32_t inputs_on_device;        /* 1: inputs/sequence_length are device (HBM) pointers
+                                      on the decoder's (root) device */
   const void* inputs;              /* [max_time, batch_size, num_classes] row-major */
   const int32_t* sequence_length;  /* [batch_size] */
-  int64_t max_time, batch_size, num_classes;
+  int64_t max_time, batch_size, num_classes;   /* inputs.dim_size(0..2) (0 past the rank) */
   int32_t beam_width;              /* attr beam_width >= 1 */
   int32_t top_paths;               /* attr top_paths >= 1 */
   int32_t merge_repeated;          /* attr merge_repeated (default false) */
@@ -60,6 +63,10 @@ typedef struct {
   int32_t blank_label;             /* attr blank_label (default -1) */
   int32_t flags;                   /* CTCEXT_FLAG_* */
   void* stream;                    /* hipStream_t; NULL = the decoder's own stream */
+  int32_t inputs_dims;             /* inputs.dims(): must be 3 (kernels.cc:111-113) */
+  int32_t sequence_length_dims;    /* sequence_length.dims(): must be 1 (kernels.cc:122-124) */
+  int64_t sequence_length_size;    /* sequence_length.dim_size(0): must equal batch_size
+                                      (kernels.cc:126-130); the number of int32 read */
 } ctcext_decode_args;
 
 /* Per top path p: sizes of decoded_indices[p] ([num_decoded, 2]),
@@ -85,23 +92,49 @@ typedef struct {
 
 typedef struct {
   int64_t literal_frames;          /* frames replayed through the literal TopN model */
-  int64_t literal_nonfinite;       /*   ... because a beam total was not finite */
-  int64_t literal_evict_tie;       /*   ... because the evicted bottom was tied */
-  int64_t literal_order_tie;       /*   ... because two surviving totals were equal */
+  int64_t literal_nonfinite;       /*   ... because a total or logit was not finite */
+  int64_t literal_fill;            /*   ... because the beam filled up mid-frame */
+  int64_t duplicate_frames;        /* frames whose beam held one entry twice (reachable
+                                      with -inf logits: decoder.h:142 + 189-199) */
   int64_t no_label_paths;          /* paths whose alignment is empty: the reference prints
                                       "No label seq available" (ctc_beam_entry.h:148-150) */
-  double decode_kernel_ms;         /* with CTCEXT_FLAG_PROFILE: last ctcx_beam_decode time */
+  double decode_kernel_ms;         /* with CTCEXT_FLAG_PROFILE: last ctcx_beam_decode time
+                                      (the slowest device of a sharded handle) */
   double norm_kernel_ms;
   double traceback_ms;             /* traceback + scan */
+  int32_t n_devices;               /* devices of the handle */
+  int32_t pad_;
 } ctcext_stats;
 
 /* Handle lifetime.  A handle owns a HIP stream and a grow-only device
- * workspace; it is not thread-safe (use one per thread, like an OpKernel). */
+ * workspace; it is not thread-safe (use one per thread, like an OpKernel).
+ * Every entry point restores the calling thread's current HIP device. */
 int ctcext_create(int device, ctcext_decoder** out);
 void ctcext_destroy(ctcext_decoder* dec);
 
+/* Multi-device handle for one process driving several GPUs: the batch is split
+ * into contiguous shards balanced by sum(sequence_length), one per device
+ * (devices[0] is the root: inputs_on_device pointers live there, and the
+ * outputs are assembled there).  Each device decodes its shard on its own
+ * stream; the per-item walks are gathered to the root over peer copies (xGMI)
+ * and packed there, so the outputs are identical to a one-device decode.  The
+ * same device may be listed twice (its shards then share its CUs).  Use it
+ * with ctcext_decode_sharded + ctcext_fetch. */
+int ctcext_create_sharded(const int* devices, int n_devices, ctcext_decoder** out);
+
+/* The reference's ValidateInputsGenerateOutputs (kernels.cc:97-139) plus this
+ * library's attribute checks, on the host only (no HIP call, no handle): the
+ * messages are the reference's verbatim and come in its order.  The
+ * sequence_length values (kernels.cc:134-139) are checked here only when they
+ * are host memory (inputs_on_device == 0); ctcext_decode checks them always. */
+int ctcext_validate(const ctcext_decode_args* args);
+
 /* Phase 1 (Compute up to the allocation of the outputs).  Synchronous. */
 int ctcext_decode(ctcext_decoder* dec, const ctcext_decode_args* args, ctcext_path_sizes* sizes);
+
+/* Phase 1 over a ctcext_create_sharded handle (kernels.cc:68-90's batch loop
+ * split across devices).  On a one-device handle it is ctcext_decode. */
+int ctcext_decode_sharded(ctcext_decoder* dec, const ctcext_decode_args* args, ctcext_path_sizes* sizes);
 
 /* Phase 2 (StoreAllDecodedSequences + log_probability).  Synchronous. */
 int ctcext_fetch(ctcext_decoder* dec, const ctcext_outputs* out);

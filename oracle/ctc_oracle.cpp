@@ -252,10 +252,13 @@ class Decoder {
 
     std::vector<N*> branches = leaves_.extract();
     leaves_.reset();
-    if (getenv("ORACLE_DUPCHECK")) {   // debugging aid: duplicate entries in the beam
+    {
+      // frames that start with one entry twice in the beam (reachable with -inf
+      // logits: decoder.h:142 pushes every branch, :189-199 re-pushes a branch
+      // that is not Active); reported so the tests can count them
       std::vector<N*> sb(branches);
       std::sort(sb.begin(), sb.end());
-      if (std::adjacent_find(sb.begin(), sb.end()) != sb.end()) printf("DUPLICATE ENTRY IN BEAM\n");
+      if (std::adjacent_find(sb.begin(), sb.end()) != sb.end()) ++dup_frames;
     }
     if (getenv("ORACLE_TRACE")) {   // debugging aid: frame-start beam, extract order
       printf("frame\n");
@@ -388,6 +391,11 @@ class Decoder {
 
   int C_, blank_, W_, blank_label_;
   Top leaves_;
+
+ public:
+  int64_t dup_frames = 0;
+
+ private:
   std::vector<std::unique_ptr<N>> pool_;
   N* root_ = nullptr;
   Store store_;
@@ -409,6 +417,7 @@ struct OracleResult {
   int32_t* dec_vals;       // concatenation over (b, p) in b-major order
   int32_t* ali_vals;
   double* log_prob;        // [B*P]
+  int64_t dup_frames;      // frames whose beam held one entry twice
 };
 
 template <class T, class Store>
@@ -428,6 +437,7 @@ static OracleResult* run(const T* x, const int32_t* seq_len, int64_t Tmax, int64
     std::vector<std::vector<int>> paths, aligns;
     std::vector<T> lps;
     int st = dec.top_paths(P, merge != 0, paths, aligns, lps, r->no_label_events);
+    r->dup_frames = dec.dup_frames;
     if (st != 0) { r->status = st; return r; }
     dec.reset();
     for (int p = 0; p < P; ++p) {

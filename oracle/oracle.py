@@ -37,7 +37,8 @@ class _Result(ctypes.Structure):
                 ("ali_len", ctypes.POINTER(ctypes.c_int64)),
                 ("dec_vals", ctypes.POINTER(ctypes.c_int32)),
                 ("ali_vals", ctypes.POINTER(ctypes.c_int32)),
-                ("log_prob", ctypes.POINTER(ctypes.c_double))]
+                ("log_prob", ctypes.POINTER(ctypes.c_double)),
+                ("dup_frames", ctypes.c_int64)]
 
 
 _lib = None
@@ -64,9 +65,11 @@ def _load():
 
 
 def raw_decode(inputs, sequence_length, beam_width, top_paths, merge_repeated=False,
-               blank_index=0, blank_label=-1, mode="shared"):
+               blank_index=0, blank_label=-1, mode="shared", stats=None):
     """Returns (dec, ali, log_prob, no_label_events) with dec[b][p] / ali[b][p]
-    python lists of ints and log_prob float64 [B, P]."""
+    python lists of ints and log_prob float64 [B, P].  ``stats`` (a dict), if
+    given, receives ``duplicate_frames``: frames that started with one entry
+    twice in the beam."""
     x = np.ascontiguousarray(inputs)
     if x.dtype not in (np.float32, np.float64):
         raise TypeError("inputs must be float32 or float64")
@@ -93,6 +96,8 @@ def raw_decode(inputs, sequence_length, beam_width, top_paths, merge_repeated=Fa
                           int(blank_label))
     try:
         res = r.contents
+        if stats is not None:
+            stats["duplicate_frames"] = int(res.dup_frames)
         if res.status == 1:
             raise OracleError("requested more paths than the beam width.")
         if res.status == 2:
@@ -142,9 +147,9 @@ def pack_sparse(seqs, B, P):
 
 
 def decode(inputs, sequence_length, beam_width, top_paths, merge_repeated=False,
-           blank_index=0, blank_label=-1, mode="shared"):
+           blank_index=0, blank_label=-1, mode="shared", stats=None):
     dec, ali, lp, _ = raw_decode(inputs, sequence_length, beam_width, top_paths,
-                                 merge_repeated, blank_index, blank_label, mode)
+                                 merge_repeated, blank_index, blank_label, mode, stats)
     B = np.asarray(inputs).shape[1]
     di, dv, ds = pack_sparse(dec, B, top_paths)
     ai, av, ash = pack_sparse(ali, B, top_paths)

@@ -1,9 +1,10 @@
 """CPU-side checks of the drop-in boundary (no GPU needed, no compute calls):
 
 * libctcext.so loads and exports every function include/ctcext.h declares;
-* the host-side validation of ctc_ext_beam_search_decoder raises the
-  reference's errors (ops.cc:12-13 attr minimums, kernels.cc:111-139 shape
-  checks) before any device work;
+* the reference's validation (ops.cc:12-13 attr minimums, kernels.cc:111-139
+  shape and length checks) runs behind the C ABI (ctcext_validate), with the
+  reference's messages in its order, before any device work -- both called
+  directly through ctypes and through the Python op;
 * without a GPU the op fails loudly (no silent CPU fallback);
 * the batch-sharded path (ctcext_amd.sharded) reassembles per-rank outputs
   into the single-device result: world_size 2 over gloo, with the oracle
@@ -77,6 +78,84 @@ def test_shape_errors_before_device_work():
     with pytest.raises(ctcext_amd.FailedPreconditionError) as e:
         ctcext_amd.ctc_ext_beam_search_decoder(np.zeros((3, 2, 4), np.float32), [3], 2, 1)
     assert e.value.message == "len(sequence_length) != batch_size.  len(sequence_length):  1 batch_size: 2"
+
+
+def _args(shape, sl, dims=None, sl_dims=1, sl_size=None, W=4, P=1, blank=0, dtype=_lib.CTCEXT_F32):
+    a = _lib.DecodeArgs()
+    a.dtype = dtype
+    a.inputs_on_device = 0
+    buf = (ctypes.c_float * 8)()
+    a.inputs = ctypes.cast(buf, ctypes.c_void_p)
+    sla = (ctypes.c_int32 * max(len(sl), 1))(*sl)
+    a.sequence_length = ctypes.cast(sla, ctypes.c_void_p)
+    d = list(shape) + [0, 0, 0]
+    a.max_time, a.batch_size, a.num_classes = d[0], d[1], d[2]
+    a.inputs_dims = len(shape) if dims is None else dims
+    a.sequence_length_dims = sl_dims
+    a.sequence_length_size = len(sl) if sl_size is None else sl_size
+    a.beam_width, a.top_paths, a.blank_index, a.blank_label = W, P, blank, -1
+    return a, (buf, sla)
+
+
+@pytest.mark.parametrize("kw,code,msg", [
+    # kernels.cc:111-113, 118-120, 122-124, 126-130, 134-139, in that order
+    (dict(shape=(3, 4), sl=[3]), _lib.CTCEXT_INVALID_ARGUMENT, "inputs is not a 3-Tensor"),
+    (dict(shape=(3, 4, 5, 6), sl=[3, 3, 3, 3]), _lib.CTCEXT_INVALID_ARGUMENT, "inputs is not a 3-Tensor"),
+    (dict(shape=(0, 1, 4), sl=[0], sl_dims=2), _lib.CTCEXT_INVALID_ARGUMENT, "max_time is 0"),
+    (dict(shape=(3, 1, 4), sl=[3], sl_dims=2), _lib.CTCEXT_INVALID_ARGUMENT, "sequence_length is not a vector"),
+    (dict(shape=(3, 1, 4), sl=[3], sl_dims=0), _lib.CTCEXT_INVALID_ARGUMENT, "sequence_length is not a vector"),
+    (dict(shape=(3, 2, 4), sl=[3]), _lib.CTCEXT_FAILED_PRECONDITION,
+     "len(sequence_length) != batch_size.  len(sequence_length):  1 batch_size: 2"),
+    (dict(shape=(3, 2, 4), sl=[3, 3, 3]), _lib.CTCEXT_FAILED_PRECONDITION,
+     "len(sequence_length) != batch_size.  len(sequence_length):  3 batch_size: 2"),
+    (dict(shape=(3, 2, 4), sl=[3, 4]), _lib.CTCEXT_FAILED_PRECONDITION, "sequence_length(1) <= 3"),
+    # attr minimums (ops.cc:12-13), then this library's checks
+    (dict(shape=(3, 1, 4), sl=[3], W=0), _lib.CTCEXT_INVALID_ARGUMENT,
+     "Value for attr 'beam_width' of 0 must be at least minimum 1"),
+    (dict(shape=(3, 1, 4), sl=[3], P=0), _lib.CTCEXT_INVALID_ARGUMENT,
+     "Value for attr 'top_paths' of 0 must be at least minimum 1"),
+    (dict(shape=(3, 1, 4), sl=[3], W=2, P=3), _lib.CTCEXT_INVALID_ARGUMENT,
+     "requested more paths than the beam width."),
+    (dict(shape=(3, 1, 4), sl=[3], blank=4), _lib.CTCEXT_INVALID_ARGUMENT,
+     "blank_index out of range [0, num_classes)"),
+    (dict(shape=(3, 1, 70000), sl=[3]), _lib.CTCEXT_UNIMPLEMENTED,
+     "num_classes 70000 exceeds the back-pointer record format (max 65535)"),
+    (dict(shape=(3, 1, 4), sl=[3], dtype=7), _lib.CTCEXT_INVALID_ARGUMENT, "dtype must be float32 or float64"),
+])
+def test_c_abi_validation(kw, code, msg):
+    # the reference's checks behind the C ABI, no GPU and no handle needed
+    lib = _lib.load()
+    a, keep = _args(**kw)
+    assert lib.ctcext_validate(ctypes.byref(a)) == code
+    assert lib.ctcext_last_error().decode() == msg
+    del keep
+
+
+def test_c_abi_validation_order_and_ok():
+    lib = _lib.load()
+    # rank is checked before everything else, length before the values
+    a, keep = _args((3, 4), [9, 9], sl_dims=2)
+    assert lib.ctcext_validate(ctypes.byref(a)) == _lib.CTCEXT_INVALID_ARGUMENT
+    assert lib.ctcext_last_error().decode() == "inputs is not a 3-Tensor"
+    a, keep = _args((3, 2, 4), [9])
+    assert lib.ctcext_validate(ctypes.byref(a)) == _lib.CTCEXT_FAILED_PRECONDITION
+    a, keep = _args((3, 2, 4), [3, 0])
+    assert lib.ctcext_validate(ctypes.byref(a)) == _lib.CTCEXT_OK
+    assert lib.ctcext_last_error().decode() == ""
+    # an empty batch is valid (no item reaches TopPaths)
+    a, keep = _args((3, 0, 4), [], W=1, P=5)
+    assert lib.ctcext_validate(ctypes.byref(a)) == _lib.CTCEXT_OK
+    del keep
+
+
+def test_unsupported_dtypes_raise_type_error():
+    # the op registers T in {float, double} only (ops.cc:17-18)
+    with pytest.raises(TypeError, match="DataType int32 not in list of allowed values: float32, float64"):
+        ctcext_amd.ctc_ext_beam_search_decoder(np.zeros((3, 1, 4), np.int32), [3], 2, 1)
+    with pytest.raises(TypeError, match="float16"):
+        ctcext_amd.ctc_ext_beam_search_decoder(np.zeros((3, 1, 4), np.float16), [3], 2, 1)
+    with pytest.raises(TypeError, match="sequence_length"):
+        ctcext_amd.ctc_ext_beam_search_decoder(np.zeros((3, 1, 4), np.float32), [3.0], 2, 1)
 
 
 @pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU behaviour")

@@ -84,17 +84,103 @@ def test_force_literal_matches_oracle():
             compare(out, ref, P)
 
 
+def _dup_frames():
+    return ctcext_amd.get_decoder(0).last_stats["duplicate_frames"]
+
+
 def test_neg_inf_logits():
     rng = np.random.default_rng(77)
+    dup_cases = 0
     for it in range(60):
         x, sl, W, P, kw = random_case(rng, neg_inf=True)
-        ref, rerr = oracle_or_error(x, sl, W, P, kw)
+        st = {}
+        try:
+            ref, rerr = oracle.decode(x, sl, W, P, stats=st, **kw), None
+        except oracle.OracleError as e:
+            ref, rerr = None, str(e)
         out, gerr = _gpu_or_error(x, sl, W, P, kw)
-        if gerr is not None and "same entry twice" in gerr:
-            continue    # documented unsupported state
         assert rerr == gerr, (it, rerr, gerr)
         if ref is not None:
             compare(out, ref, P)
+            assert _dup_frames() == st["duplicate_frames"], it
+            dup_cases += st["duplicate_frames"] > 0
+    print("neg-inf cases whose beam held an entry twice: %d of 60" % dup_cases)
+
+
+def _dup_family(seed, n_want, dtype=np.float32, max_tries=4000):
+    """Seeded single-item -inf-heavy cases that the oracle reports reaching the
+    duplicate-entry state (decoder.h:142 pushes every branch, :189-199 re-pushes
+    a non-Active branch as a child, so one BeamEntry sits in the beam twice)."""
+    rng = np.random.default_rng(seed)
+    got = []
+    for _ in range(max_tries):
+        T = int(rng.integers(2, 30)); C = int(rng.integers(2, 8)); W = int(rng.integers(1, 10))
+        x = rng.standard_normal((T, 1, C)).astype(dtype)
+        x[rng.random(x.shape) < (0.3 if rng.random() < 0.5 else 0.5)] = -np.inf
+        P = int(rng.integers(1, W + 1))
+        kw = dict(merge_repeated=bool(rng.integers(2)), blank_index=int(rng.integers(C)),
+                  blank_label=int(rng.integers(-1, C)))
+        st = {}
+        try:
+            ref = oracle.decode(x, [T], W, P, stats=st, **kw)
+        except oracle.OracleError:
+            continue
+        if st["duplicate_frames"]:
+            got.append((x, np.array([T], np.int32), W, P, kw, ref, st["duplicate_frames"]))
+            if len(got) == n_want:
+                break
+    assert len(got) == n_want
+    return got
+
+
+@pytest.mark.parametrize("dtype,flags", [(np.float32, 0), (np.float64, 0),
+                                         (np.float32, _lib.CTCEXT_FLAG_FORCE_LITERAL)])
+def test_duplicate_entry_state(dtype, flags):
+    # the reference's beam holding one BeamEntry twice, reproduced bit-exactly:
+    # second roll empties old_cands, second recursion accumulates, shared
+    # children (ctcx_decode.hip literal_step); the device counts the same
+    # number of duplicate frames as the oracle
+    for k, (x, sl, W, P, kw, ref, nd) in enumerate(_dup_family(31337, 30, dtype)):
+        out, err = _gpu_or_error(x, sl, W, P, kw, flags=flags)
+        assert err is None, (k, err)
+        compare(out, ref, P)
+        assert _dup_frames() == nd, (k, _dup_frames(), nd)
+
+
+def test_duplicate_entry_batch_with_finite_items():
+    # duplicate items next to ordinary items in one batch (per-item state)
+    rng = np.random.default_rng(1)
+    for (x, sl, W, P, kw, _, nd) in _dup_family(4242, 6):
+        Tb = x.shape[0]
+        big = rng.standard_normal((Tb, 3, x.shape[2])).astype(np.float32)
+        big[:, 1] = x[:, 0]
+        slb = np.array([Tb, Tb, max(Tb - 3, 0)], np.int32)
+        st = {}
+        ref = oracle.decode(big, slb, W, P, stats=st, **kw)
+        out, err = _gpu_or_error(big, slb, W, P, kw, device=True)
+        assert err is None, err
+        compare(out, ref, P)
+        assert _dup_frames() == st["duplicate_frames"]
+
+
+def test_cfg1_exact_workload():
+    # BASELINE configs[0]: B=2, T=50, C=6, beam_width=4, top_paths=1, the reference's
+    # CPU plumbing case, on both input distributions of BASELINE.md
+    rng = np.random.default_rng(20251015)
+    x = rng.standard_normal((50, 2, 6), dtype=np.float32)
+    sl = np.full(2, 50, np.int32)
+    kw = dict(merge_repeated=False, blank_index=0, blank_label=-1)
+    ref = oracle.decode(x, sl, 4, 1, **kw)
+    for device in (False, True):
+        out, err = _gpu_or_error(x, sl, 4, 1, kw, device=device)
+        assert err is None, err
+        compare(out, ref, 1)
+    hot = np.where(rng.random((50, 2)) < 0.6, 0, rng.integers(1, 6, size=(50, 2)))
+    xb = x.copy()
+    np.put_along_axis(xb, hot[..., None], np.take_along_axis(xb, hot[..., None], 2) + 6, 2)
+    out, err = _gpu_or_error(xb, sl, 4, 1, kw)
+    assert err is None, err
+    compare(out, oracle.decode(xb, sl, 4, 1, **kw), 1)
 
 
 def test_cfg2_shape_parity():

@@ -1,0 +1,119 @@
+"""Multi-device paths on the GPU (kernels.cc:68-90's batch loop split across
+devices).
+
+* ctcext_create_sharded (one process, several devices, peer-copy gather to
+  the root) must give exactly the one-device outputs and the oracle's.  The
+  box has one GPU, so the device list names it twice: the shards then run on
+  two streams of the same GPU, which exercises the split, the strided input
+  copies and the gather, not xGMI.
+* one process per GPU (ctcext_amd.sharded.gather_to_root): two ranks started
+  by torch.distributed.run as a child process (never an exec of this
+  GPU-initialised process), each decoding its shard with the HIP decoder on
+  cuda:0 and gathering over gloo (RCCL refuses two ranks on one device); rank 0
+  writes the gathered outputs, compared here with the one-device decode.
+* every entry point restores the caller's current device.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+import ctcext_amd
+import oracle
+from parity_util import compare, to_numpy
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _same(a, b, P):
+    for p in range(P):
+        for k in a._fields[:-1]:
+            np.testing.assert_array_equal(to_numpy(getattr(a, k)[p]), to_numpy(getattr(b, k)[p]),
+                                          err_msg="%s[%d]" % (k, p))
+    np.testing.assert_array_equal(to_numpy(a.log_probability), to_numpy(b.log_probability))
+
+
+@pytest.mark.parametrize("B,device_in,ragged", [(5, True, True), (5, False, True), (1, True, False),
+                                                (4, True, False), (7, False, False)])
+def test_sharded_handle_matches_single_device(B, device_in, ragged):
+    rng = np.random.default_rng(100 + B)
+    T, C, W, P = 120, 29, 32, 2
+    x = rng.standard_normal((T, B, C)).astype(np.float32)
+    sl = (rng.integers(0, T + 1, size=B) if ragged else np.full(B, T)).astype(np.int32)
+    kw = dict(merge_repeated=True, blank_index=0, blank_label=-1)
+    xin = torch.as_tensor(x, device="cuda:0") if device_in else x
+    slin = torch.as_tensor(sl, device="cuda:0") if device_in else sl
+    one = ctcext_amd.ctc_ext_beam_search_decoder(xin, slin, W, P, **kw)
+    for devs in ([0, 0], [0, 0, 0]):
+        many = ctcext_amd.ctc_ext_beam_search_decoder(xin, slin, W, P, devices=devs, **kw)
+        assert ctcext_amd.get_decoder(tuple(devs)).last_stats["n_devices"] == len(devs)
+        _same(many, one, P)
+    compare(one, oracle.decode(x, sl, W, P, **kw), P)
+
+
+def test_sharded_handle_large_c_and_f64():
+    rng = np.random.default_rng(7)
+    x = rng.standard_normal((40, 6, 300))
+    sl = np.array([40, 12, 1, 40, 33, 1], np.int32)
+    kw = dict(merge_repeated=False, blank_index=5, blank_label=-1)
+    one = ctcext_amd.ctc_ext_beam_search_decoder(x, sl, 16, 3, **kw)
+    many = ctcext_amd.ctc_ext_beam_search_decoder(x, sl, 16, 3, devices=[0, 0, 0, 0], **kw)
+    _same(many, one, 3)
+    compare(one, oracle.decode(x, sl, 16, 3, **kw), 3)
+    # zero-length items (top_paths 1: the root is the only leaf) in some shards
+    sl0 = np.array([40, 0, 0, 40, 0, 7], np.int32)
+    one = ctcext_amd.ctc_ext_beam_search_decoder(x, sl0, 16, 1, **kw)
+    many = ctcext_amd.ctc_ext_beam_search_decoder(x, sl0, 16, 1, devices=[0, 0, 0, 0], **kw)
+    _same(many, one, 1)
+    compare(one, oracle.decode(x, sl0, 16, 1, **kw), 1)
+
+
+def test_sharded_handle_errors_match():
+    x = np.random.default_rng(0).standard_normal((5, 3, 4)).astype(np.float32)
+    for devs in (None, [0, 0]):
+        with pytest.raises(ctcext_amd.InvalidArgumentError) as e:
+            ctcext_amd.ctc_ext_beam_search_decoder(x[:1], [1, 1, 1], 10, 5, devices=devs)
+        assert e.value.message == "Less leaves in the beam search than requested."
+        with pytest.raises(ctcext_amd.FailedPreconditionError) as e:
+            ctcext_amd.ctc_ext_beam_search_decoder(x, [6, 1, 1], 4, 1, devices=devs)
+        assert e.value.message == "sequence_length(0) <= 5"
+
+
+def test_current_device_is_restored():
+    # the C ABI saves and restores the caller's HIP device (torch reads the
+    # same runtime's current device)
+    n = torch.cuda.device_count()
+    x = np.random.default_rng(0).standard_normal((10, 2, 5)).astype(np.float32)
+    for cur in range(min(n, 2)):
+        torch.cuda.set_device(cur)
+        ctcext_amd.ctc_ext_beam_search_decoder(torch.as_tensor(x, device="cuda:0"), [10, 10], 4, 1)
+        assert torch.cuda.current_device() == cur
+        ctcext_amd.ctc_ext_beam_search_decoder(x, [10, 10], 4, 1, devices=[0, 0])
+        assert torch.cuda.current_device() == cur
+    torch.cuda.set_device(0)
+
+
+def test_two_ranks_hip_decoder_gather(tmp_path):
+    out = str(tmp_path / "rank0.npz")
+    port = 29500 + (os.getpid() % 2000)
+    env = dict(os.environ, CTCX_ONE_DEVICE="1", PYTHONUNBUFFERED="1",
+               HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=%d" % port,
+           os.path.join(ROOT, "tests", "dist_worker.py"), out]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    got = np.load(out)
+    import dist_worker
+    x, sl, W, P, kw = dist_worker.workload()
+    one = ctcext_amd.ctc_ext_beam_search_decoder(x, sl, W, P, **kw)
+    for p in range(P):
+        for k in one._fields[:-1]:
+            np.testing.assert_array_equal(got["%s_%d" % (k, p)], to_numpy(getattr(one, k)[p]),
+                                          err_msg="%s[%d]" % (k, p))
+    np.testing.assert_array_equal(got["log_probability"], to_numpy(one.log_probability))
