@@ -86,7 +86,8 @@ def cpu_share():
 def algorithmic_bytes(sl, C, P, out, tsize=4):
     """logits read + seq_len + int64 SparseTensor components +
     shapes + log_prob, from the actual output sizes."""
-    n = sum(int(out.decoded_values[p].numel()) + int(out.alignment_values[p].numel()) for p in range(P))
+    n = sum(int(np.prod(out.decoded_values[p].shape)) + int(np.prod(out.alignment_values[p].shape))
+            for p in range(P))
     B = len(sl)
     return int(np.sum(sl, dtype=np.int64)) * C * tsize + 4 * B + 24 * n + 32 * P + B * P * tsize
 

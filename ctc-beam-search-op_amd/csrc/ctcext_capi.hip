@@ -106,7 +106,7 @@ struct Dev {
   hipStream_t own_stream = nullptr;
   hipStream_t s = nullptr;   // stream of the current call
   hipEvent_t ev[4] = {};
-  DevBuf x, sl, norm, rec, item, top_pos, top_kind, logp, seq, len, phase;
+  DevBuf x, sl, norm, rec, item, top_pos, top_kind, logp, seq, len, phase, sctab;
   int64_t lo = 0, nb = 0;    // this call's shard [lo, lo + nb)
 };
 
@@ -130,7 +130,7 @@ static void release_dev(Dev& d) {
   (void)hipSetDevice(d.device);
   if (d.own_stream) (void)hipStreamSynchronize(d.own_stream);
   DevBuf* bufs[] = {&d.x, &d.sl, &d.norm, &d.rec, &d.item, &d.top_pos, &d.top_kind, &d.logp,
-                    &d.seq, &d.len, &d.phase};
+                    &d.seq, &d.len, &d.phase, &d.sctab};
   for (DevBuf* b : bufs) b->release();
   for (auto& ev : d.ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -138,12 +138,16 @@ static void release_dev(Dev& d) {
   d.own_stream = nullptr;
 }
 
-extern "C" int32_t ctcext_max_beam_width(int64_t num_classes, int32_t dtype) {
+static int32_t max_beam_width(int64_t num_classes, int32_t dtype, bool scored) {
   const int ts = dtype == CTCEXT_F64 ? 8 : 4;
   int lo = 0;
   for (int w = 1; w <= 512; ++w)
-    if (ctcx::decode_lds_bytes(w, num_classes, ts) <= ctcx::kLdsBytes) lo = w;
+    if (ctcx::decode_lds_bytes(w, num_classes, ts, scored) <= ctcx::kLdsBytes) lo = w;
   return lo;
+}
+
+extern "C" int32_t ctcext_max_beam_width(int64_t num_classes, int32_t dtype) {
+  return max_beam_width(num_classes, dtype, false);
 }
 
 extern "C" int ctcext_create_sharded(const int* devices, int n_devices, ctcext_decoder** out) {
@@ -244,7 +248,27 @@ static int validate_shapes(const ctcext_decode_args* a) {
                                                 std::to_string(a->sequence_length_size) +
                                                 " batch_size: " + std::to_string(B));
   if (B > 0 && (!a->inputs || !a->sequence_length)) return fail(CTCEXT_INVALID_ARGUMENT, "null input pointer");
+  if (a->scorer != CTCEXT_SCORER_BASE && a->scorer != CTCEXT_SCORER_BIGRAM)
+    return fail(CTCEXT_INVALID_ARGUMENT, "unknown beam scorer");
+  if (a->scorer == CTCEXT_SCORER_BIGRAM && B > 0 && !a->scorer_table)
+    return fail(CTCEXT_INVALID_ARGUMENT, "bigram beam scorer without a table");
   return CTCEXT_OK;
+}
+
+// The bigram table's entries must be log-probabilities: <= 0 and not NaN
+// (exact_step's skipping bounds a child's score by its parent's total).
+template <typename T>
+static int check_table_t(const T* t, int64_t n) {
+  for (int64_t i = 0; i < n; ++i)
+    if (!(t[i] <= T(0)))
+      return fail(CTCEXT_INVALID_ARGUMENT, "beam scorer table entries must be log-probabilities (<= 0)");
+  return CTCEXT_OK;
+}
+static int check_table(const ctcext_decode_args* a, const void* host_table) {
+  if (a->scorer != CTCEXT_SCORER_BIGRAM || a->batch_size == 0) return CTCEXT_OK;
+  const int64_t n = (a->num_classes + 1) * a->num_classes;
+  return a->dtype == CTCEXT_F64 ? check_table_t((const double*)host_table, n)
+                                : check_table_t((const float*)host_table, n);
 }
 
 // kernels.cc:133-139
@@ -269,7 +293,7 @@ static int check_limits(const ctcext_decode_args* a) {
     return fail(CTCEXT_UNIMPLEMENTED, "num_classes " + std::to_string(C) +
                                           " exceeds the back-pointer record format (max " +
                                           std::to_string(ctcx::kMaxRecClasses) + ")");
-  const int wmax = ctcext_max_beam_width(C, a->dtype);
+  const int wmax = max_beam_width(C, a->dtype, a->scorer != CTCEXT_SCORER_BASE);
   if (a->beam_width > wmax)
     return fail(CTCEXT_UNIMPLEMENTED, "beam_width " + std::to_string(a->beam_width) + " with num_classes " +
                                           std::to_string(C) + " exceeds the LDS-resident beam state (max " +
@@ -285,6 +309,7 @@ extern "C" int ctcext_validate(const ctcext_decode_args* a) {
     if (rc != CTCEXT_OK) return rc;
   }
   rc = check_limits(a);
+  if (rc == CTCEXT_OK && !a->inputs_on_device) rc = check_table(a, a->scorer_table);
   if (rc == CTCEXT_OK) g_err.clear();
   return rc;
 }
@@ -352,6 +377,13 @@ static int enqueue_shard(ctcext_decoder* d, Dev& v, bool root, const ctcext_deco
   p.top_kind = (int32_t*)v.top_kind.p;
   p.log_prob = (T*)v.logp.p;
   p.prof = nullptr;
+  p.scorer_tab = nullptr;
+  if (a->scorer == CTCEXT_SCORER_BIGRAM) {   // each device reads its own copy
+    const size_t tb = (size_t)((C + 1) * C) * sizeof(T);
+    HIP_OR_FAIL(v.sctab.ensure(tb));
+    HIP_OR_FAIL(hipMemcpyAsync(v.sctab.p, a->scorer_table, tb, hipMemcpyDefault, s));
+    p.scorer_tab = (const T*)v.sctab.p;
+  }
   if (a->flags & CTCEXT_FLAG_PHASES) {
     HIP_OR_FAIL(v.phase.ensure(8 * ctcx::kPhaseN * (size_t)Bs));
     p.prof = (uint64_t*)v.phase.p;
@@ -512,6 +544,16 @@ extern "C" int ctcext_decode_sharded(ctcext_decoder* d, const ctcext_decode_args
   }
   rc = check_lengths(hsl.data(), B, T_);
   if (rc == CTCEXT_OK) rc = check_limits(a);
+  if (rc == CTCEXT_OK && a->scorer == CTCEXT_SCORER_BIGRAM && B > 0) {
+    if (a->inputs_on_device) {
+      const size_t tb = (size_t)((a->num_classes + 1) * a->num_classes) * (a->dtype == CTCEXT_F64 ? 8 : 4);
+      std::vector<char> ht(tb);
+      HIP_OR_FAIL(hipMemcpy(ht.data(), a->scorer_table, tb, hipMemcpyDeviceToHost));
+      rc = check_table(a, ht.data());
+    } else {
+      rc = check_table(a, a->scorer_table);
+    }
+  }
   if (rc != CTCEXT_OK) return rc;
 
   const int P = a->top_paths;

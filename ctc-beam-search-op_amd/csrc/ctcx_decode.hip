@@ -182,6 +182,9 @@ struct Ctx {
   CTCX_LDS int* htab;
   CTCX_LDS uint64_t* bloom;   // per branch: label bits (l & 63) of children evicted this frame
   CTCX_LDS HE<T>* he;  // TopN elements_, position p at he[p + 1]
+  // beam-scorer state (a stateful scorer only): per branch [buf][i], per entry
+  CTCX_LDS T* est[2]; CTCX_LDS T* eest;
+  const T* sctab;      // the scorer's table (global memory)
   int W, C, blank, enc, hts, wcap;
 };
 
@@ -220,7 +223,7 @@ constexpr uint64_t kRootHa = 0x243F6A8885A308D3ull, kRootHb = 0x13198A2E03707344
 // compile-time Wcap all of them are instruction immediates instead of ~45
 // pointer SGPRs.  decode_lds_bytes (ctcx_kernels.h) mirrors this sum.
 template <typename T>
-__host__ __device__ void carve(Ctx<T>& cx, CTCX_LDS char* base, int Wcap, int W, int C) {
+__host__ __device__ void carve(Ctx<T>& cx, CTCX_LDS char* base, int Wcap, int W, int C, bool scored = false) {
   const size_t ENC = 3 * (size_t)Wcap + 2;
   auto a16 = [](size_t v) { return (v + 15) & ~(size_t)15; };
   CTCX_LDS char* p = base;
@@ -268,10 +271,45 @@ __host__ __device__ void carve(Ctx<T>& cx, CTCX_LDS char* base, int Wcap, int W,
   p += a16(8 * (size_t)Wcap);
   cx.he = (CTCX_LDS HE<T>*)p;
   p += ((size_t)Wcap + 2 + 64) * sizeof(HE<T>);
+  cx.est[0] = cx.est[1] = cx.eest = nullptr;
+  if (scored) {
+    cx.est[0] = (CTCX_LDS T*)p; cx.est[1] = cx.est[0] + Wcap; cx.eest = cx.est[1] + Wcap;
+    p += a16((2 * (size_t)Wcap + ENC) * sizeof(T));
+  }
   cx.row = (CTCX_LDS T*)p;
   cx.wcap = Wcap;
   cx.W = W; cx.C = C; cx.enc = (int)ENC;
 }
+
+// ---------------------------------------------------------------------------
+// Beam scorer hook (util/ctc_beam_scorer.h:31-65), a compile-time policy.  The
+// decoder calls InitializeState on the root (decoder.h:226), ExpandState when a
+// child is (re)created in the grow loop (:171) and GetStateExpansionScore on the
+// previous-frame score it extends (recursion :103, :114; grow :176, :182).
+// ExpandStateEnd / GetStateEndExpansionScore are never called by this decoder
+// (TopPaths, :230-261, does not), so the policies have no such members.
+// A state is one T per beam (the cached expansion score, as the reference's
+// comment suggests).  Scores must be log-probabilities (<= 0): the exact
+// skipping in exact_step bounds a child's score by its parent's total.
+
+// BaseBeamScorer, the scorer the reference op uses (kernels.cc:260): identity.
+template <typename T>
+struct BaseBeamScorer {
+  static constexpr bool kStateful = false;
+  __host__ __device__ static T expand(const Ctx<T>&, T, int, int) { return T(0); }
+  __host__ __device__ static T score(T, T prev) { return prev; }
+};
+
+// A bigram expansion score: ExpandState caches table[from_label + 1][to_label]
+// (row 0: expansions of the root, label -1); GetStateExpansionScore adds it.
+template <typename T>
+struct BigramBeamScorer {
+  static constexpr bool kStateful = true;
+  __host__ __device__ static T expand(const Ctx<T>& cx, T, int from_label, int to_label) {
+    return cx.sctab[(int64_t)(from_label + 1) * cx.C + to_label];
+  }
+  __host__ __device__ static T score(T state, T prev) { return prev + state; }
+};
 
 // Alignment candidate "from S.kind" for a receiver (ctc_beam_entry.h:190-228).
 // restart: the base probability when S has no candidate of that kind.
@@ -289,7 +327,7 @@ __host__ __device__ __forceinline__ void cand_from(const Ctx<T>& cx, int buf, in
 // whose entry is its first occurrence's).  Reads the frame-start branch arrays
 // and the entry's current newp (rolled = oldp, except in literal mode where a
 // parent processed earlier, or an earlier occurrence, may have changed it).
-template <typename T>
+template <typename T, class SC>
 __host__ __device__ __forceinline__ void recurse_branch(const Ctx<T>& cx, int buf, int i, int e, T norm,
                                                         bool literal) {
   const T NI = ninf<T>();
@@ -309,7 +347,8 @@ __host__ __device__ __forceinline__ void recurse_branch(const Ctx<T>& cx, int bu
     const bool pactive = (P >= 0) && (!literal || cx.et[P] != NI);
     if (pactive) {
       const bool same = (L == sel(cx.lab, buf)[P]);
-      const T prev = same ? sel(cx.ob, buf)[P] : sel(cx.ot, buf)[P];
+      T prev = same ? sel(cx.ob, buf)[P] : sel(cx.ot, buf)[P];
+      if constexpr (SC::kStateful) prev = SC::score(sel(cx.est, buf)[i], prev);
       nl = lse(nl, prev) + xl - norm;
       cand_from(cx, buf, P, 0, p, rs_blank, bn);
       if (!same) cand_from(cx, buf, P, 1, p, NI, bn);
@@ -341,6 +380,7 @@ __host__ __device__ __forceinline__ void recurse_branch(const Ctx<T>& cx, int bu
   cx.eflg[e] = (bb.ok ? F_HB : 0) | (bn.ok ? F_HN : 0);
   cx.ekind[e] = ((uint32_t)e << 1);
   cx.elab[e] = L;
+  if constexpr (SC::kStateful) cx.eest[e] = sel(cx.est, buf)[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -681,7 +721,7 @@ __device__ HE<T> wave_first_min_to_front(CTCX_LDS HE<T>* he, int n) {
 // then peeks lazily; rare: only while the beam is still filling).
 // On success cx.sorted[0..*n_out) holds the Extract() order and, for the last
 // frame, cx.tops[0..min(P, leaves)) the TopPaths() selection as positions.
-template <typename T, int RN, bool BIG>
+template <typename T, int RN, bool BIG, class SC>
 __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, bool last, int P, int* n_out,
                           int* n_leaves, uint64_t* pc) {
   uint64_t ts0 = pc ? __builtin_amdgcn_s_memtime() : 0;
@@ -726,7 +766,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     cx.bloom[i] = 0;
   }
   __syncthreads();
-  for (int i = lane; i < nb; i += 64) recurse_branch(cx, buf, i, i, norm, false);
+  for (int i = lane; i < nb; i += 64) recurse_branch<T, SC>(cx, buf, i, i, norm, false);
   __syncthreads();
   bool nonfinite = false;
   for (int i = lane; i < nb; i += 64) {
@@ -894,7 +934,13 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     bool live = valid && !(cx.bst[i] & S_DEACT);
     const T xl = cx.row[l];
     const T p = xl - norm;
-    const T s = p + ((l == bl) ? sel(cx.ob, buf)[i] : bt);
+    T base = (l == bl) ? sel(cx.ob, buf)[i] : bt;
+    T cst = T(0);   // the child's scorer state (ExpandState, decoder.h:171)
+    if constexpr (SC::kStateful) {
+      cst = SC::expand(cx, sel(cx.est, buf)[i], bl, l);
+      base = SC::score(cst, base);
+    }
+    const T s = p + base;
     // the lane where this lane's branch turn starts in the chunk (< 0: in an
     // earlier chunk, found open there), and the bottom at that moment (bat:
     // refreshed after every event for turns that start later in the chunk)
@@ -1091,6 +1137,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       cx.eflg[myslot] = F_HN;
       cx.ekind[myslot] = isbc ? ((uint32_t)c << 1) : (((uint32_t)i << 1) | 1u);
       cx.elab[myslot] = l;
+      if constexpr (SC::kStateful) cx.eest[myslot] = cst;
       if (isbc) __hip_atomic_fetch_and(&cx.bst[c], ~S_EVICT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 #ifdef CTCX_FASTLOOP_PROF
@@ -1174,7 +1221,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
 // Positions holding the same entry are linked by cx.alias (the first
 // occurrence, which owns the entry slot); dup_in says this frame has any, and
 // *dup_out that the next one does.
-template <typename T>
+template <typename T, class SC>
 __host__ __device__ __attribute__((noinline)) int literal_step(Ctx<T> cx, int buf, int nb, T norm, bool last, int P,
                                                                bool dup_in, int* dup_out, int* n_leaves) {
   const T NI = ninf<T>();
@@ -1201,7 +1248,7 @@ __host__ __device__ __attribute__((noinline)) int literal_step(Ctx<T> cx, int bu
 
   for (int i = 0; i < nb; ++i) {
     const int a = dup_in ? cx.alias[i] : i;
-    recurse_branch(cx, buf, i, a, norm, true);
+    recurse_branch<T, SC>(cx, buf, i, a, norm, true);
     lit_top_push(h, a, gt);
   }
 
@@ -1238,7 +1285,12 @@ __host__ __device__ __attribute__((noinline)) int literal_step(Ctx<T> cx, int bu
       const T xl = cx.row[l];
       const T p = xl - norm;
       cx.eb[slot] = NI;
-      const T prev = (l == bl) ? sel(cx.ob, buf)[i] : sel(cx.ot, buf)[i];
+      T prev = (l == bl) ? sel(cx.ob, buf)[i] : sel(cx.ot, buf)[i];
+      if constexpr (SC::kStateful) {
+        const T cst = SC::expand(cx, sel(cx.est, buf)[i], bl, l);   // ExpandState (decoder.h:171)
+        cx.eest[slot] = cst;
+        prev = SC::score(cst, prev);
+      }
       cx.el[slot] = xl - norm + prev;
       const bool recv_fresh = fresh_slot ? true : (sel(cx.ot, buf)[c] == NI);
       const T rs_blank = ((bflg & F_ROOT) && recv_fresh) ? T(0) : NI;
@@ -1305,12 +1357,13 @@ __host__ __device__ __attribute__((noinline)) int literal_step(Ctx<T> cx, int bu
 }
 
 // ---------------------------------------------------------------------------
-template <typename T, int RN, int WC, bool BIG>
+template <typename T, int RN, int WC, bool BIG, class SC>
 __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   Ctx<T> cx;
-  carve(cx, (CTCX_LDS char*)lds, WC > 0 ? WC : prm.W, prm.W, (int)prm.C);
+  carve(cx, (CTCX_LDS char*)lds, WC > 0 ? WC : prm.W, prm.W, (int)prm.C, SC::kStateful);
   cx.blank = prm.blank;
+  cx.sctab = prm.scorer_tab;
   const int lane = threadIdx.x;
   const int64_t b = blockIdx.x;
   const int W = prm.W;
@@ -1328,6 +1381,7 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     cx.ha[0][0] = kRootHa; cx.hb[0][0] = kRootHb; cx.pha[0][0] = 0; cx.phb[0][0] = 0;
     cx.head[0] = -1;
     cx.alias[0] = 0;
+    if constexpr (SC::kStateful) cx.est[0][0] = T(0);   // InitializeState (decoder.h:226)
   }
   int nb = 1;
   int literal_steps = 0;
@@ -1359,7 +1413,7 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     uint64_t t1 = prof ? __builtin_amdgcn_s_memtime() : 0;
     if (prof) pc[0] += t1 - t0;
     if (!prm.force_literal && !dup)
-      why = exact_step<T, RN, BIG>(cx, buf, nb, norm, last, prm.P, &n, &nl_fast, prof ? pc : nullptr);
+      why = exact_step<T, RN, BIG, SC>(cx, buf, nb, norm, last, prm.P, &n, &nl_fast, prof ? pc : nullptr);
     __syncthreads();
     uint64_t t2 = prof ? __builtin_amdgcn_s_memtime() : 0;
     const bool ok = (why == 0);
@@ -1369,13 +1423,13 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     if (!ok) {
       if (lane == 0) {
         int d2 = 0, nl = 0;
-        misc[0] = literal_step(cx, buf, nb, norm, last, prm.P, dup, &d2, &nl);
+        misc[0] = literal_step<T, SC>(cx, buf, nb, norm, last, prm.P, dup, &d2, &nl);
         misc[1] = d2;
         misc[2] = nl;
       }
       __syncthreads();
       n = misc[0];
-      dup_next = misc[1] != 0;
+      dup_next = uni(misc[1]) != 0;   // wave-uniform: the next frame's exact_step call stays uniform
       n_leaves = misc[2];
       ++literal_steps;
     } else {
@@ -1455,6 +1509,7 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
       sel(cx.flg, nx)[k] = fl;
       sel(cx.ot, nx)[k] = cx.et[e]; sel(cx.ob, nx)[k] = cx.eb[e]; sel(cx.ol, nx)[k] = cx.el[e];
       sel(cx.cb, nx)[k] = cx.ecb[e]; sel(cx.cn, nx)[k] = cx.ecn[e];
+      if constexpr (SC::kStateful) sel(cx.est, nx)[k] = cx.eest[e];
       rout[k] = rec_pack(kd, cx.elab[e], (ef & F_HB) ? cx.ebpb[e] : kBpNone, (ef & F_HN) ? cx.ebpn[e] : kBpNone);
     }
     __syncthreads();
@@ -1635,24 +1690,24 @@ __global__ __launch_bounds__(64) void ctcx_pack(PackParams pp) {
 // Launchers (called by the C-ABI layer).
 namespace ctcx {
 
-template <typename T, int RN, int WC, bool BIG>
+template <typename T, int RN, int WC, bool BIG, class SC>
 static hipError_t launch_decode_c(const DecodeParams<T>& p, hipStream_t s) {
-  const size_t lds = decode_lds_bytes(WC > 0 ? WC : p.W, p.C, (int)sizeof(T));
+  const size_t lds = decode_lds_bytes(WC > 0 ? WC : p.W, p.C, (int)sizeof(T), SC::kStateful);
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)ctcx_beam_decode<T, RN, WC, BIG>,
+    hipError_t e = hipFuncSetAttribute((const void*)ctcx_beam_decode<T, RN, WC, BIG, SC>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((ctcx_beam_decode<T, RN, WC, BIG>), dim3((unsigned)p.B), dim3(64), lds, s, p);
+  hipLaunchKernelGGL((ctcx_beam_decode<T, RN, WC, BIG, SC>), dim3((unsigned)p.B), dim3(64), lds, s, p);
   return hipGetLastError();
 }
 
 // BIG (C > 64): the grow loop's branch/window skipping by row-block maxima is
 // compiled in; small-C builds keep the leaner loop (its register allocation is
 // what cfg3 runs on)
-template <typename T, int RN, int WC>
+template <typename T, int RN, int WC, class SC = BaseBeamScorer<T>>
 static hipError_t launch_decode_r(const DecodeParams<T>& p, hipStream_t s) {
-  return p.C > 64 ? launch_decode_c<T, RN, WC, true>(p, s) : launch_decode_c<T, RN, WC, false>(p, s);
+  return p.C > 64 ? launch_decode_c<T, RN, WC, true, SC>(p, s) : launch_decode_c<T, RN, WC, false, SC>(p, s);
 }
 
 template <typename T>
@@ -1660,6 +1715,12 @@ hipError_t launch_decode(const DecodeParams<T>& p, hipStream_t s) {
   if (p.B == 0) return hipSuccess;
   // RN registers per lane hold the min-child of the (W + 1) / 2 internal heap
   // nodes; the compile-time layouts (WC) are used whenever they fit the LDS
+  if (p.scorer_tab) {   // the bigram scorer: runtime LDS layout only
+    using SC = BigramBeamScorer<T>;
+    if (p.W <= 128) return launch_decode_r<T, 1, 0, SC>(p, s);
+    if (p.W <= 256) return launch_decode_r<T, 2, 0, SC>(p, s);
+    return launch_decode_r<T, 4, 0, SC>(p, s);
+  }
   auto fits = [&](int wc) { return decode_lds_bytes(wc, p.C, (int)sizeof(T)) <= kLdsBytes; };
   if (p.W <= 128) return fits(128) ? launch_decode_r<T, 1, 128>(p, s) : launch_decode_r<T, 1, 0>(p, s);
   if (p.W <= 256) return fits(256) ? launch_decode_r<T, 2, 256>(p, s) : launch_decode_r<T, 2, 0>(p, s);

@@ -73,6 +73,7 @@ struct DecodeParams {
   int32_t* top_kind;        // [B][P]  0 blank / 1 label-ending / -1 none
   T* log_prob;              // [B][P]
   uint64_t* prof;           // optional [B][8] phase cycle counters (diagnostics)
+  const T* scorer_tab;      // bigram beam-scorer table [C + 1][C], or null (BaseBeamScorer)
 };
 
 struct TraceParams {
@@ -110,7 +111,7 @@ constexpr size_t kLdsBytes = 160 * 1024;   // LDS per CU on gfx950 (one workgrou
 
 // Bytes of the decode kernel's LDS layout for a beam capacity W (carve() in
 // ctcx_decode.hip, same order and alignment).
-__host__ __device__ inline size_t decode_lds_bytes(int W, int64_t C, int tsize) {
+__host__ __device__ inline size_t decode_lds_bytes(int W, int64_t C, int tsize, bool scored = false) {
   const size_t ENC = 3 * (size_t)W + 2;
   auto a16 = [](size_t v) { return (v + 15) & ~(size_t)15; };
   size_t s = 0;
@@ -128,6 +129,7 @@ __host__ __device__ inline size_t decode_lds_bytes(int W, int64_t C, int tsize) 
   s += a16(4 * (size_t)htab_size(W));           // per-frame new-leaf hash table
   s += a16(8 * (size_t)W);                      // per-branch evicted-child label bloom
   s += ((size_t)W + 2 + 64) * (tsize == 8 ? 16 : 8); // TopN elements (value, slot) + per-lane dummy slots
+  if (scored) s += a16((2 * (size_t)W + ENC) * tsize); // beam-scorer states (branches x2, entries)
   s += a16((size_t)C * tsize);                  // logit row
   s += a16((size_t)((C + 63) / 64) * tsize);    // its per-64-label block maxima
   return s;

@@ -22,6 +22,8 @@ CTCEXT_F64 = 1
 CTCEXT_FLAG_FORCE_LITERAL = 1
 CTCEXT_FLAG_PROFILE = 2
 CTCEXT_FLAG_PHASES = 4
+CTCEXT_SCORER_BASE = 0
+CTCEXT_SCORER_BIGRAM = 1
 
 # every symbol include/ctcext.h declares
 EXPORTED_SYMBOLS = ("ctcext_create", "ctcext_create_sharded", "ctcext_destroy", "ctcext_validate",
@@ -39,7 +41,8 @@ class DecodeArgs(ctypes.Structure):
                 ("blank_label", ctypes.c_int32), ("flags", ctypes.c_int32),
                 ("stream", ctypes.c_void_p),
                 ("inputs_dims", ctypes.c_int32), ("sequence_length_dims", ctypes.c_int32),
-                ("sequence_length_size", ctypes.c_int64)]
+                ("sequence_length_size", ctypes.c_int64),
+                ("scorer", ctypes.c_int32), ("pad_", ctypes.c_int32), ("scorer_table", ctypes.c_void_p)]
 
 
 class PathSizes(ctypes.Structure):

@@ -197,7 +197,7 @@ def _args(x_ptr, shape, dtype_code, on_device, sl_ptr, sl_shape, beam_width, top
 
 def ctc_ext_beam_search_decoder(inputs, sequence_length, beam_width, top_paths,
                                 merge_repeated=False, blank_index=0, blank_label=-1,
-                                name=None, *, flags=0, outputs="auto", devices=None):
+                                name=None, *, flags=0, outputs="auto", devices=None, scorer_table=None):
     """Drop-in for the reference op.  See the module docstring.
 
     Keyword-only extensions (not in the reference):
@@ -207,6 +207,11 @@ def ctc_ext_beam_search_decoder(inputs, sequence_length, beam_width, top_paths,
       devices: a list of device ordinals to decode contiguous batch shards on,
         in one process (ctcext_create_sharded); device inputs must live on
         devices[0], where the outputs are assembled.
+      scorer_table: a [num_classes + 1, num_classes] table of log-probabilities
+        (<= 0) for the decoder's beam-scorer hook (util/ctc_beam_scorer.h:31-65):
+        expanding a beam that ends in label a (row 0: the empty beam) by label
+        b adds table[a + 1, b] to the score it extends.  The reference op
+        always uses the identity scorer (kernels.cc:260), which None selects.
       flags: CTCEXT_FLAG_* diagnostics.
     """
     del name
@@ -256,6 +261,21 @@ def ctc_ext_beam_search_decoder(inputs, sequence_length, beam_width, top_paths,
         stream = None
     a = _args(x_ptr, shape, code, on_device, sl_ptr, sl_shape, beam_width, top_paths, merge_repeated,
               blank_index, blank_label, flags, stream)
+    if scorer_table is not None:
+        C = int(shape[2]) if len(shape) == 3 else 0
+        if on_device:
+            import torch
+            tab = torch.as_tensor(scorer_table, device=x.device, dtype=x.dtype).contiguous()
+            a.scorer_table = tab.data_ptr()
+        else:
+            tab = np.ascontiguousarray(np.asarray(
+                scorer_table.detach().cpu().numpy() if _is_torch(scorer_table) else scorer_table, dtype=x.dtype))
+            a.scorer_table = tab.ctypes.data
+        if tuple(tab.shape) != (C + 1, C):
+            raise ValueError("scorer_table must be [num_classes + 1, num_classes] = [%d, %d], got %s"
+                             % (C + 1, C, tuple(tab.shape)))
+        keep.append(tab)
+        a.scorer = _lib.CTCEXT_SCORER_BIGRAM
     # the reference's shape/length checks run behind the C ABI, before any
     # device work (kernels.cc:97-139)
     rc = lib.ctcext_validate(ctypes.byref(a))

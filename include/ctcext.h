@@ -38,6 +38,15 @@ enum {
 
 enum { CTCEXT_F32 = 0, CTCEXT_F64 = 1 };   /* attr T: {float, double} (ops.cc:24) */
 
+/* Beam scorer (util/ctc_beam_scorer.h:31-65).  The reference op always uses
+ * BaseBeamScorer (kernels.cc:260), the identity; the decoder exposes the hook
+ * (ctc_ext_beam_search_decoder.h:43-45, 103, 114, 171-182, 226).
+ *   CTCEXT_SCORER_BIGRAM: ExpandState caches table[from_label + 1][to_label]
+ *   (row 0: expansions of the root), GetStateExpansionScore adds it to the
+ *   score it extends.  table is [num_classes + 1][num_classes] of dtype, in
+ *   the memory inputs_on_device says; entries are log-probabilities (<= 0). */
+enum { CTCEXT_SCORER_BASE = 0, CTCEXT_SCORER_BIGRAM = 1 };
+
 enum {
   CTCEXT_FLAG_FORCE_LITERAL = 1,   /* testing: replay every frame through the literal TopN model */
   CTCEXT_FLAG_PROFILE = 2,         /* time the decode kernel with HIP events (ctcext_stats) */
@@ -67,6 +76,9 @@ typedef struct {
   int32_t sequence_length_dims;    /* sequence_length.dims(): must be 1 (kernels.cc:122-124) */
   int64_t sequence_length_size;    /* sequence_length.dim_size(0): must equal batch_size
                                       (kernels.cc:126-130); the number of int32 read */
+  int32_t scorer;                  /* CTCEXT_SCORER_* (0: the reference op's BaseBeamScorer) */
+  int32_t pad_;
+  const void* scorer_table;        /* CTCEXT_SCORER_BIGRAM: [num_classes + 1][num_classes] */
 } ctcext_decode_args;
 
 /* Per top path p: sizes of decoded_indices[p] ([num_decoded, 2]),

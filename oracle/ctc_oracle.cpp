@@ -23,6 +23,9 @@
 //   * Step / Reset / TopPaths                 util/ctc_ext_beam_search_decoder.h:66-261
 //   * Compute batch driver, validation, SparseTensor packing
 //                                             kernels/ctc_ext_beam_search_decoder_kernels.cc:20-257
+//   * beam scorer hook (BaseBeamScorer identity, or a bigram expansion-score
+//     table)                                   util/ctc_beam_scorer.h:31-65, used at
+//                                              ctc_ext_beam_search_decoder.h:103, 114, 171-182, 226
 //   * gtl::TopN (third-party, TensorFlow tensorflow/core/lib/gtl/top_n.h,
 //     TF 1.14-2.1 era per configure.sh:59-81): restated from its published
 //     algorithm — UNORDERED -> BOTTOM_KNOWN -> HEAP_SORTED, libstdc++
@@ -208,6 +211,7 @@ struct Node {
   std::unordered_map<int, Node*> kids;
   T old_t = LogZero<T>(), old_b = LogZero<T>(), old_l = LogZero<T>();
   T new_t = LogZero<T>(), new_b = LogZero<T>(), new_l = LogZero<T>();
+  T state = T(0);   // beam-scorer state: the cached expansion score
   typename Store::Slots old_c, new_c;
   Node(Node* p, int l) : parent(p), label(l) {}
   bool active() const { return new_t != LogZero<T>(); }
@@ -227,8 +231,10 @@ class Decoder {
   using Top = BoundedTop<N*, NodeGreater<T, Store>>;
 
  public:
-  Decoder(int C, int blank_index, int W, int blank_label)
-      : C_(C), blank_(blank_index), W_(W), blank_label_(blank_label), leaves_(W) { reset(); }
+  // tab: bigram scorer table [C + 1][C] (row from_label + 1), or null for
+  // BaseBeamScorer (the identity the reference op uses, kernels.cc:260)
+  Decoder(int C, int blank_index, int W, int blank_label, const T* tab = nullptr)
+      : C_(C), blank_(blank_index), W_(W), blank_label_(blank_label), leaves_(W), tab_(tab) { reset(); }
 
   void reset() {
     leaves_.reset();
@@ -239,6 +245,7 @@ class Decoder {
     root_->new_t = T(0);
     root_->new_b = T(0);
     leaves_.push(root_);
+    root_->state = T(0);   // InitializeState (decoder.h:226)
   }
 
   // ctc_ext_beam_search_decoder.h:69-210
@@ -285,7 +292,7 @@ class Decoder {
         if (P->active()) {
           const bool same = (b->label == P->label);
           const T prev = same ? P->old_b : P->old_t;
-          b->new_l = LSE(b->new_l, prev) + x[b->label] - norm;
+          b->new_l = LSE(b->new_l, expansion_score(b, prev)) + x[b->label] - norm;
           cand(b, 1, P, 0, p, b->label);
           if (!same) cand(b, 1, P, 1, p, b->label);
           cand(b, 1, b, 1, p, b->label);
@@ -309,11 +316,12 @@ class Decoder {
         if (c->active()) continue;
         const T p = x[l] - norm;
         c->new_b = LogZero<T>();
+        expand_state(b, c, l);
         if (l == b->label) {
-          c->new_l = x[l] - norm + b->old_b;
+          c->new_l = x[l] - norm + expansion_score(c, b->old_b);
           cand(c, 1, b, 0, p, l);
         } else {
-          c->new_l = x[l] - norm + b->old_t;
+          c->new_l = x[l] - norm + expansion_score(c, b->old_t);
           cand(c, 1, b, 0, p, l);
           cand(c, 1, b, 1, p, l);
         }
@@ -361,6 +369,12 @@ class Decoder {
   }
 
  private:
+  // ctc_beam_scorer.h:41-56: ExpandState / GetStateExpansionScore
+  void expand_state(const N* from, N* to, int to_label) {
+    if (tab_) to->state = tab_[(int64_t)(from->label + 1) * C_ + to_label];
+  }
+  T expansion_score(const N* n, T prev) const { return tab_ ? prev + n->state : prev; }
+
   bool admissible(T total) {
     return total > LogZero<T>() &&
            (leaves_.size() < (size_t)W_ || total > leaves_.peek_bottom()->new_t);
@@ -391,6 +405,7 @@ class Decoder {
 
   int C_, blank_, W_, blank_label_;
   Top leaves_;
+  const T* tab_;
 
  public:
   int64_t dup_frames = 0;
@@ -422,12 +437,12 @@ struct OracleResult {
 
 template <class T, class Store>
 static OracleResult* run(const T* x, const int32_t* seq_len, int64_t Tmax, int64_t B, int64_t C,
-                         int W, int P, int merge, int blank_index, int blank_label) {
+                         int W, int P, int merge, int blank_index, int blank_label, const T* tab) {
   OracleResult* r = new OracleResult();
   memset(r, 0, sizeof(*r));
   std::vector<std::vector<int>> dec_all, ali_all;
   std::vector<double> lp(B * P, 0.0);
-  oracle::Decoder<T, Store> dec((int)C, blank_index, W, blank_label);
+  oracle::Decoder<T, Store> dec((int)C, blank_index, W, blank_label, tab);
   std::vector<T> row(C);
   for (int64_t b = 0; b < B; ++b) {
     for (int64_t t = 0; t < seq_len[b]; ++t) {
@@ -468,18 +483,27 @@ static OracleResult* run(const T* x, const int32_t* seq_len, int64_t Tmax, int64
 
 extern "C" {
 
-// dtype 0 = float32, 1 = float64; mode 0 = faithful store, 1 = shared store.
+// dtype 0 = float32, 1 = float64; mode 0 = faithful store, 1 = shared store;
+// table: bigram beam-scorer table [C + 1][C] of dtype, or null (BaseBeamScorer).
+OracleResult* oracle_decode_scored(int dtype, int mode, const void* x, const int32_t* seq_len,
+                                   int64_t T, int64_t B, int64_t C, int W, int P, int merge,
+                                   int blank_index, int blank_label, const void* table) {
+  if (dtype == 0) {
+    const float* xf = (const float*)x;
+    const float* tf = (const float*)table;
+    return mode == 0 ? run<float, oracle::FaithfulStore<float>>(xf, seq_len, T, B, C, W, P, merge, blank_index, blank_label, tf)
+                     : run<float, oracle::SharedStore<float>>(xf, seq_len, T, B, C, W, P, merge, blank_index, blank_label, tf);
+  }
+  const double* xd = (const double*)x;
+  const double* td = (const double*)table;
+  return mode == 0 ? run<double, oracle::FaithfulStore<double>>(xd, seq_len, T, B, C, W, P, merge, blank_index, blank_label, td)
+                   : run<double, oracle::SharedStore<double>>(xd, seq_len, T, B, C, W, P, merge, blank_index, blank_label, td);
+}
+
 OracleResult* oracle_decode(int dtype, int mode, const void* x, const int32_t* seq_len,
                             int64_t T, int64_t B, int64_t C, int W, int P, int merge,
                             int blank_index, int blank_label) {
-  if (dtype == 0) {
-    const float* xf = (const float*)x;
-    return mode == 0 ? run<float, oracle::FaithfulStore<float>>(xf, seq_len, T, B, C, W, P, merge, blank_index, blank_label)
-                     : run<float, oracle::SharedStore<float>>(xf, seq_len, T, B, C, W, P, merge, blank_index, blank_label);
-  }
-  const double* xd = (const double*)x;
-  return mode == 0 ? run<double, oracle::FaithfulStore<double>>(xd, seq_len, T, B, C, W, P, merge, blank_index, blank_label)
-                   : run<double, oracle::SharedStore<double>>(xd, seq_len, T, B, C, W, P, merge, blank_index, blank_label);
+  return oracle_decode_scored(dtype, mode, x, seq_len, T, B, C, W, P, merge, blank_index, blank_label, nullptr);
 }
 
 void oracle_free(OracleResult* r) {

@@ -59,17 +59,21 @@ def _load():
             ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
             ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
             ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        lib.oracle_decode_scored.restype = ctypes.POINTER(_Result)
+        lib.oracle_decode_scored.argtypes = lib.oracle_decode.argtypes + [ctypes.c_void_p]
         lib.oracle_free.argtypes = [ctypes.POINTER(_Result)]
         _lib = lib
     return _lib
 
 
 def raw_decode(inputs, sequence_length, beam_width, top_paths, merge_repeated=False,
-               blank_index=0, blank_label=-1, mode="shared", stats=None):
+               blank_index=0, blank_label=-1, mode="shared", stats=None, scorer_table=None):
     """Returns (dec, ali, log_prob, no_label_events) with dec[b][p] / ali[b][p]
     python lists of ints and log_prob float64 [B, P].  ``stats`` (a dict), if
     given, receives ``duplicate_frames``: frames that started with one entry
-    twice in the beam."""
+    twice in the beam.  ``scorer_table`` ([C + 1, C], the inputs' dtype): the
+    bigram beam scorer (see ctc_oracle.cpp); None is the reference op's
+    BaseBeamScorer."""
     x = np.ascontiguousarray(inputs)
     if x.dtype not in (np.float32, np.float64):
         raise TypeError("inputs must be float32 or float64")
@@ -90,10 +94,15 @@ def raw_decode(inputs, sequence_length, beam_width, top_paths, merge_repeated=Fa
     if not 0 <= blank_index < C:
         raise OracleError("blank_index out of range")
     lib = _load()
-    r = lib.oracle_decode(0 if x.dtype == np.float32 else 1, 0 if mode == "faithful" else 1,
-                          x.ctypes.data, sl.ctypes.data, T, B, C, int(beam_width),
-                          int(top_paths), int(bool(merge_repeated)), int(blank_index),
-                          int(blank_label))
+    tab = None
+    if scorer_table is not None:
+        tab = np.ascontiguousarray(np.asarray(scorer_table, dtype=x.dtype))
+        if tab.shape != (C + 1, C):
+            raise ValueError("scorer_table must be [num_classes + 1, num_classes]")
+    r = lib.oracle_decode_scored(0 if x.dtype == np.float32 else 1, 0 if mode == "faithful" else 1,
+                                 x.ctypes.data, sl.ctypes.data, T, B, C, int(beam_width),
+                                 int(top_paths), int(bool(merge_repeated)), int(blank_index),
+                                 int(blank_label), None if tab is None else tab.ctypes.data)
     try:
         res = r.contents
         if stats is not None:
@@ -147,9 +156,9 @@ def pack_sparse(seqs, B, P):
 
 
 def decode(inputs, sequence_length, beam_width, top_paths, merge_repeated=False,
-           blank_index=0, blank_label=-1, mode="shared", stats=None):
+           blank_index=0, blank_label=-1, mode="shared", stats=None, scorer_table=None):
     dec, ali, lp, _ = raw_decode(inputs, sequence_length, beam_width, top_paths,
-                                 merge_repeated, blank_index, blank_label, mode, stats)
+                                 merge_repeated, blank_index, blank_label, mode, stats, scorer_table)
     B = np.asarray(inputs).shape[1]
     di, dv, ds = pack_sparse(dec, B, top_paths)
     ai, av, ash = pack_sparse(ali, B, top_paths)

@@ -397,3 +397,79 @@ def test_large_vocab_golden(name):
             np.testing.assert_array_equal(got.reshape(exp.shape), exp, err_msg="%s[%d]" % (k, p))
     lp = np.asarray([[float.fromhex(h) for h in row] for row in fx["log_probability_hex"]], np.float32)
     np.testing.assert_array_equal(to_numpy(out.log_probability), lp)
+
+
+# ---- beam-scorer hook (util/ctc_beam_scorer.h:31-65).  Parity unpinned: the
+# reference op always runs BaseBeamScorer (kernels.cc:260), so the bigram
+# scorer's only checker is the oracle's restatement of the hook call sites
+# (decoder.h:103, 114, 171-182, 226).
+
+def _bigram(rng, C, dtype, scale=2.0, sparse=False):
+    tab = -np.abs(rng.standard_normal((C + 1, C))) * scale
+    if sparse:   # mostly free transitions, a few penalised ones
+        tab[rng.random(tab.shape) < 0.8] = 0.0
+    return tab.astype(dtype)
+
+
+def _run_scored(seed, n, dtype=np.float32, flags=0, device=False, **kw_case):
+    rng = np.random.default_rng(seed)
+    for it in range(n):
+        x, sl, W, P, kw = random_case(rng, dtype=dtype, **kw_case)
+        tab = _bigram(rng, x.shape[2], dtype, sparse=bool(it % 2))
+        try:
+            ref, rerr = oracle.decode(x, sl, W, P, scorer_table=tab, **kw), None
+        except oracle.OracleError as e:
+            ref, rerr = None, str(e)
+        try:
+            if device:
+                import torch
+                out = ctcext_amd.ctc_ext_beam_search_decoder(
+                    torch.as_tensor(x, device="cuda"), torch.as_tensor(sl, device="cuda"), W, P,
+                    flags=flags, scorer_table=torch.as_tensor(tab, device="cuda"), **kw)
+            else:
+                out = ctcext_amd.ctc_ext_beam_search_decoder(x, sl, W, P, flags=flags, scorer_table=tab, **kw)
+            gerr = None
+        except ctcext_amd.OpError as e:
+            out, gerr = None, e.message
+        assert rerr == gerr, (it, rerr, gerr)
+        if ref is not None:
+            compare(out, ref, P)
+
+
+def test_scorer_random_small():
+    _run_scored(6001, 120)
+    _run_scored(6002, 60, ties=True)
+
+
+def test_scorer_f64_literal_device():
+    _run_scored(6003, 40, dtype=np.float64)
+    _run_scored(6004, 30, flags=_lib.CTCEXT_FLAG_FORCE_LITERAL)
+    _run_scored(6005, 20, device=True, T_max=80, C_max=30, W_max=40)
+
+
+def test_scorer_large_c_and_neg_inf():
+    # large C runs the skip scans, whose bounds need scores <= 0
+    _run_scored(6006, 12, T_max=30, B_max=2, C_min=65, C_max=300, W_max=100, scale=4.0)
+    _run_scored(6007, 30, neg_inf=True)
+
+
+def test_scorer_zero_table_is_identity():
+    rng = np.random.default_rng(6008)
+    x = rng.standard_normal((200, 3, 29)).astype(np.float32)
+    sl = np.array([200, 150, 199], np.int32)
+    kw = dict(merge_repeated=True, blank_index=0, blank_label=-1)
+    base = ctcext_amd.ctc_ext_beam_search_decoder(x, sl, 64, 3, **kw)
+    zero = ctcext_amd.ctc_ext_beam_search_decoder(x, sl, 64, 3, scorer_table=np.zeros((30, 29), np.float32), **kw)
+    compare(zero, oracle.decode(x, sl, 64, 3, **kw), 3)
+    compare(base, oracle.decode(x, sl, 64, 3, **kw), 3)
+
+
+def test_scorer_rejects_positive_scores():
+    x = np.zeros((3, 1, 4), np.float32)
+    tab = np.zeros((5, 4), np.float32)
+    tab[2, 1] = 0.5
+    with pytest.raises(ctcext_amd.InvalidArgumentError) as e:
+        ctcext_amd.ctc_ext_beam_search_decoder(x, [3], 2, 1, scorer_table=tab)
+    assert "log-probabilities" in e.value.message
+    with pytest.raises(ValueError):
+        ctcext_amd.ctc_ext_beam_search_decoder(x, [3], 2, 1, scorer_table=np.zeros((4, 4), np.float32))

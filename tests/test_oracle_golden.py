@@ -67,3 +67,27 @@ def test_oracle_errors():
         oracle.decode(np.zeros((0, 1, 3), np.float32), [0], 2, 1)
     with pytest.raises(oracle.OracleError, match=r"sequence_length\(0\) <= 4"):
         oracle.decode(x, [5], 2, 1)
+
+
+def test_oracle_scorer_hook():
+    """The bigram beam-scorer hook of the oracle (ctc_beam_scorer.h:31-65): an
+    all-zero table is the identity (prev + 0 == prev), so it must reproduce the
+    BaseBeamScorer decode exactly; a non-trivial table must change the search.
+    (Parity unpinned: the reference op never exposes a scorer, kernels.cc:260.)"""
+    rng = np.random.default_rng(9)
+    x = rng.standard_normal((30, 2, 6)).astype(np.float32)
+    sl = [30, 22]
+    kw = dict(merge_repeated=True, blank_index=0, blank_label=-1)
+    base = oracle.decode(x, sl, 8, 2, **kw)
+    zero = oracle.decode(x, sl, 8, 2, scorer_table=np.zeros((7, 6), np.float32), **kw)
+    for f in base._fields:
+        for a, b in zip(getattr(base, f), getattr(zero, f)):
+            np.testing.assert_array_equal(a, b)
+    tab = -np.abs(rng.standard_normal((7, 6))).astype(np.float32) * 3
+    lm = oracle.decode(x, sl, 8, 2, scorer_table=tab, **kw)
+    assert not np.array_equal(lm.log_probability, base.log_probability)
+    # the faithful (reference-cost) store agrees with the shared one under a scorer too
+    lmf = oracle.decode(x, sl, 8, 2, scorer_table=tab, mode="faithful", **kw)
+    for f in lm._fields:
+        for a, b in zip(getattr(lm, f), getattr(lmf, f)):
+            np.testing.assert_array_equal(a, b)
