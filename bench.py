@@ -230,8 +230,12 @@ def main():
         else:
             traffic_src = "stale: %s is of build %s, this is %s" % (os.path.relpath(pmc, ROOT),
                                                                    pj.get("lib_sha16"), lib_hash())
+    metric = "decoded frames/sec at B=256, T=1500, C=29, beam_width=128; 1/2/4/8 GPUs"   # BASELINE.json
+    if args.config != "cfg3" or args.seq_len:   # diagnostics lines name their own workload
+        metric = "decoded frames/sec at B=%d, T=%d, C=%d, beam_width=%d (%s, not the BASELINE metric)" % (
+            B * world, T, C, W, args.config)
     res = {
-        "metric": "decoded frames/sec at B=256, T=1500, C=29, beam_width=128; 1/2/4/8 GPUs",
+        "metric": metric,
         "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32",

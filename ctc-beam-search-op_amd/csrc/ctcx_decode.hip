@@ -1562,30 +1562,73 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
 }
 
 // ---------------------------------------------------------------------------
-// Softmax normaliser per row (decoder.h:72-80): max, sequential sum of
-// exp(x - max) in T precision, log.  Rows past an item's length are skipped.
 // Softmax normaliser per (t, b) row (decoder.h:72-80): sequential max, then a
 // sequential sum of exp(x_j - max) in class order, norm = max + log(sum), with
-// T's libm (float: expf/logf; double: exp/log), one thread per row.
+// T's libm (float: expf/logf; double: exp/log).  Rows past an item's length
+// are skipped.  The sums stay one thread per row (the reference's order), but
+// the row data reaches the threads through LDS: one wave owns 64 consecutive
+// rows and stages them in 64-class tiles, each tile row read as one coalesced
+// 64-lane load (HBM-bound; the first build read C strided values per thread
+// and reached ~0.2 TB/s).  Two passes over the tiles (max, then sum); for
+// C <= 64 the row stays in LDS between them.
 __host__ __device__ __forceinline__ float norm_exp(float x) { return gm::expf(x); }
 __host__ __device__ __forceinline__ double norm_exp(double x) { return gm::exp(x); }
 __host__ __device__ __forceinline__ float norm_log(float x) { return gm::logf(x); }
 __host__ __device__ __forceinline__ double norm_log(double x) { return gm::log(x); }
 
+constexpr int kNormTile = 64;
+
 template <typename T>
-__global__ __launch_bounds__(256) void ctcx_row_norm(const T* __restrict__ x, const int32_t* seq_len,
-                                                    T* __restrict__ norm, int64_t Tmax, int64_t B, int64_t C,
-                                                    int64_t xstride) {
-  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (row >= Tmax * B) return;
-  const int64_t t = row / B, b = row - t * B;
-  if (t >= seq_len[b]) return;
-  const T* r = x + (t * xstride + b) * C;
-  T m = r[0];
-  for (int64_t j = 1; j < C; ++j) m = (r[j] > m) ? r[j] : m;
-  T s = T(0);
-  for (int64_t j = 0; j < C; ++j) s += norm_exp(r[j] - m);
-  norm[row] = m + norm_log(s);
+__global__ __launch_bounds__(64) void ctcx_row_norm(const T* __restrict__ x, const int32_t* seq_len,
+                                                   T* __restrict__ norm, int64_t Tmax, int64_t B, int64_t C,
+                                                   int64_t xstride) {
+  __shared__ T tile[64][kNormTile + 1];   // [row in wave][class in tile], padded: conflict-free row reads
+  const int lane = threadIdx.x;
+  const int64_t rows = Tmax * B;
+  const int64_t r0 = (int64_t)blockIdx.x * 64;
+  const int64_t row = r0 + lane;
+  bool valid = false;
+  int64_t off = 0;   // this lane's row, in elements of x
+  if (row < rows) {
+    const int64_t t = row / B, b = row - t * B;
+    valid = t < seq_len[b];
+    if (valid) off = (t * xstride + b) * C;
+  }
+  const uint64_t vmask = __ballot(valid);
+  if (vmask == 0) return;
+  T m = T(0), s = T(0);
+  for (int pass = 0; pass < 2; ++pass) {
+    for (int64_t c0 = 0; c0 < C; c0 += kNormTile) {
+      const int nc = (int)(C - c0 < kNormTile ? C - c0 : kNormTile);
+      if (pass == 0 || C > kNormTile) {
+        __syncthreads();
+        // row rr of the tile: one load per lane, sizeof(T) * nc contiguous
+        // bytes; all 64 loads are issued before the first LDS write (an
+        // invalid row reads x's first row instead and is never used)
+        T v[64];
+        const int col = lane < nc ? (int)c0 + lane : 0;
+#pragma unroll
+        for (int rr = 0; rr < 64; ++rr) {
+          const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)off, rr);
+          const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)off >> 32), rr);
+          v[rr] = x[(int64_t)(((uint64_t)hi << 32) | lo) + col];
+        }
+#pragma unroll
+        for (int rr = 0; rr < 64; ++rr) tile[rr][lane] = v[rr];
+        __syncthreads();
+      }
+      if (valid) {
+        if (pass == 0) {
+          int j = 0;
+          if (c0 == 0) { m = tile[lane][0]; j = 1; }
+          for (; j < nc; ++j) { const T v = tile[lane][j]; m = (v > m) ? v : m; }
+        } else {
+          for (int j = 0; j < nc; ++j) s += norm_exp(tile[lane][j] - m);
+        }
+      }
+    }
+  }
+  if (valid) norm[row] = m + norm_log(s);
 }
 
 // ---------------------------------------------------------------------------
@@ -1735,7 +1778,7 @@ hipError_t launch_row_norm(const T* x, const int32_t* sl, T* norm, int64_t T_, i
                            int64_t xstride, hipStream_t s) {
   const int64_t rows = T_ * B;
   if (rows == 0) return hipSuccess;
-  hipLaunchKernelGGL(ctcx_row_norm<T>, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, s, x, sl, norm, T_, B, C,
+  hipLaunchKernelGGL(ctcx_row_norm<T>, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, s, x, sl, norm, T_, B, C,
                      xstride);
   return hipGetLastError();
 }

@@ -5,9 +5,12 @@
 // Why it exists: when two beam totals are exactly equal, WHICH entry is the
 // bottom (evicted) and the order in which branches are visited next frame
 // depend on the heap layout produced by libstdc++'s make_heap / pop_heap /
-// sort_heap / introsort.  The fast GPU path (ctcx_decode.hip) detects such
-// ties and replays the frame through this literal model, run by one lane over
-// LDS arrays.  Elements are slot ids; the comparator reads each slot's CURRENT
+// sort_heap / introsort.  The fast GPU path (ctcx_decode.hip exact_step)
+// replays that heap layout itself, wave-parallel; this literal model, run by
+// one lane over LDS arrays, serves the frames the fast path does not model
+// (non-finite totals, the beam filling up mid-frame, an entry held twice), the
+// unsorted-layout TopN(n) of TopPaths, and std::sort for a frame whose beam
+// never overflowed.  Elements are slot ids; the comparator reads each slot's CURRENT
 // total (the reference compares through BeamEntry pointers, so an entry
 // modified while inside the heap is seen with its new value — e.g. the
 // evicted bottom whose total is reset to -inf before the push).

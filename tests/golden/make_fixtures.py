@@ -29,6 +29,9 @@ CASES = {
     "cfg4_like_T60_B2_P3": (4002, 60, 2, 1000, 64, 3, True, 17, -1, [60, 41]),
     "cfg5_like_T30": (5001, 30, 1, 5000, 256, 1, False, 0, -1, [30]),
     "cfg5_like_T20_P2_blank_last": (5002, 20, 1, 5000, 256, 2, True, 4999, 4999, [20]),
+    # longer items (round 2): the large-C skip scans over many more frames
+    "cfg4_like_T400_B2": (4003, 400, 2, 1000, 64, 1, False, 0, -1, [400, 377]),
+    "cfg5_like_T100": (5003, 100, 1, 5000, 256, 1, False, 0, -1, [100]),
 }
 
 

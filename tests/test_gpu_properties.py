@@ -128,6 +128,30 @@ def test_cfg2_full_size_properties():
 
 
 @pytest.mark.parametrize("cfg", ["cfg4", "cfg5"])
+def test_large_vocab_full_size_properties(cfg):
+    # cfg4 per-GPU shard (B=128 of 1024 over 8 GPUs, T=2000, C=1000, W=64) and
+    # cfg5 whole (B=512, T=3000, C=5000, W=256, blank_index=0: 30.7 GB of
+    # logits, drawn on the device) at full length; ragged lengths U[T/2, T]
+    if cfg == "cfg4":
+        B, T, C, W, P = 128, 2000, 1000, 64, 1
+    else:
+        B, T, C, W, P = 512, 3000, 5000, 256, 1
+    g = torch.Generator(device="cuda")
+    g.manual_seed(4000 if cfg == "cfg4" else 5000)
+    x = torch.randn((T, B, C), generator=g, device="cuda", dtype=torch.float32)
+    sl_np = np.random.default_rng(9).integers(T // 2, T + 1, size=B).astype(np.int32)
+    sl_np[:2] = T
+    sl = torch.as_tensor(sl_np, device="cuda")
+    full = _decode(x, sl, W, P, False)
+    _check_structure(full, sl_np, C, P, False)
+    lo, n = B // 2 - 3, 8
+    part = _decode(x[:, lo:lo + n].contiguous(), sl[lo:lo + n].contiguous(), W, P, False)
+    _assert_same_rows(full, part, lo, n, P)
+    del x
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("cfg", ["cfg4", "cfg5"])
 def test_large_vocab_shape_properties(cfg):
     # cfg4 (C=1000, W=64) and cfg5 (C=5000, W=256, blank_index=0) per-GPU
     # shapes on a shortened T (the full T runs in bench.py --config)

@@ -1,0 +1,87 @@
+// fetch_calib.hip — calibrates rocprofv3's FETCH_SIZE / WRITE_SIZE on gfx950
+// for the access patterns of this repository's kernels, against known byte
+// counts (MI355X_MICROARCH.md: FETCH_SIZE reads 1/2 of the bytes of a 16 B/lane
+// streaming read; other widths are uncalibrated).
+//
+//   hipcc --offload-arch=gfx950 -O3 tools/fetch_calib.hip -o tools/fetch_calib
+//   rocprofv3 --pmc FETCH_SIZE --output-format csv -d OUT -o run -- tools/fetch_calib
+//   rocprofv3 --pmc WRITE_SIZE --output-format csv -d OUT -o run -- tools/fetch_calib
+//   python tools/pmc_calib.py OUT/.../counter_collection.csv  (ratios per kernel)
+//
+// Kernels (each launched 3 times over a fresh 44.5 MB buffer = the cfg3 logits,
+// T=1500 x B=256 x C=29 float32; bytes per launch printed to stdout):
+//   calib_stream16   16 B per lane, fully coalesced (the guide's control case)
+//   calib_rows       the decode kernel's row load: workgroup b (one wave64)
+//                    loops over t and lanes < C read row (t, b), 4 B per lane
+//                    (rows of neighbouring items share 128-B lines and run on
+//                    different XCDs)
+//   calib_rec_store  the decode kernel's record store: 8 B per lane, W = 128
+//                    records per (item, frame) (cfg3: 393 MB)
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#define CK(x)                                                                   \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                  \
+    }                                                                           \
+  } while (0)
+
+__global__ __launch_bounds__(256) void calib_stream16(const float4* __restrict__ x, size_t n4, float* out) {
+  float acc = 0.f;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+    const float4 v = x[i];
+    acc += v.x + v.y + v.z + v.w;
+  }
+  if (acc == 12345.f) out[0] = acc;   // keeps the loads, never true for N(0,1)-ish data
+}
+
+__global__ __launch_bounds__(64) void calib_rows(const float* __restrict__ x, int T, int B, int C, float* out) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  float acc = 0.f;
+  for (int t = 0; t < T; ++t) {
+    const float* r = x + ((size_t)t * B + b) * C;
+    if (lane < C) acc += r[lane];
+  }
+  if (acc == 12345.f) out[b] = acc;
+}
+
+__global__ __launch_bounds__(64) void calib_rec_store(unsigned long long* __restrict__ rec, int T, int W) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  for (int t = 0; t < T; ++t) {
+    unsigned long long* r = rec + ((size_t)b * T + t) * W;
+    for (int k = lane; k < W; k += 64) r[k] = ((unsigned long long)t << 32) | (unsigned)k;
+  }
+}
+
+int main() {
+  const int T = 1500, B = 256, C = 29, W = 128;
+  const size_t n = (size_t)T * B * C;
+  const size_t bytes = n * 4;
+  float* x;
+  float* out;
+  unsigned long long* rec;
+  CK(hipMalloc(&x, bytes));
+  CK(hipMalloc(&out, 4096 * 4));
+  CK(hipMalloc(&rec, (size_t)B * T * W * 8));
+  float* h = (float*)malloc(bytes);
+  for (size_t i = 0; i < n; ++i) h[i] = (float)((i * 2654435761u) % 1000) * 1e-3f;
+  for (int rep = 0; rep < 3; ++rep) {
+    CK(hipMemcpy(x, h, bytes, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(calib_stream16, dim3(2048), dim3(256), 0, 0, (const float4*)x, bytes / 16, out);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(x, h, bytes, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(calib_rows, dim3(B), dim3(64), 0, 0, x, T, B, C, out);
+    CK(hipDeviceSynchronize());
+    hipLaunchKernelGGL(calib_rec_store, dim3(B), dim3(64), 0, 0, rec, T, W);
+    CK(hipDeviceSynchronize());
+  }
+  printf("{\"calib_stream16\": %zu, \"calib_rows\": %zu, \"calib_rec_store_write\": %zu}\n", bytes / 16 * 16, bytes,
+         (size_t)B * T * W * 8);
+  free(h);
+  return 0;
+}

@@ -1,47 +1,70 @@
-"""Per-launch HBM bytes of the decode kernel from two rocprofv3 counter passes.
+"""Per-launch HBM bytes of the decode kernel from two rocprofv3 counter passes,
+stamped with the library build they measured.
 
-usage: python tools/pmc_summary.py FETCH.csv WRITE.csv [config] > profiles/pmc_<config>.json
+usage: python tools/pmc_summary.py FETCH.csv WRITE.csv CONFIG SEQ_LEN CALIB_FETCH.csv CALIB_WRITE.csv CALIB.json
+       > profiles/pmc_<CONFIG>.json
 
 FETCH.csv / WRITE.csv are the counter_collection.csv files of
-  rocprofv3 --pmc FETCH_SIZE --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu
-  rocprofv3 --pmc WRITE_SIZE --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu
-(separate passes: the two do not fit one TCC pass).  Values are KB per
-dispatch; FETCH_SIZE is doubled per MI355X_MICROARCH.md (gfx950 tallies each
-128-B read request at 64 B), WRITE_SIZE is used as read.
+  rocprofv3 --pmc FETCH_SIZE --output-format csv -- python3 bench.py --config CONFIG --steps 2 --warmup 1 --no-cpu
+  rocprofv3 --pmc WRITE_SIZE --output-format csv -- python3 bench.py --config CONFIG --steps 2 --warmup 1 --no-cpu
+(separate passes: the two do not fit one TCC pass).  Values are KB per dispatch.
+
+Unit correction: MI355X_MICROARCH.md calibrates FETCH_SIZE only for 16 B/lane
+streaming reads (it reports 1/2 of the bytes).  The decode kernel reads its
+logit rows at 4 B/lane (C*4-byte rows, neighbouring items' rows sharing 128-B
+lines on different XCDs) and stores 8 B/lane records, so the factors applied
+here come from tools/fetch_calib.hip, which replays exactly those two access
+patterns over known byte counts in the same two counter passes
+(CALIB_*.csv; CALIB.json is its stdout).  factor = known bytes / counter bytes.
 """
 import csv
+import hashlib
 import json
+import os
 import sys
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "ctc-beam-search-op_amd", "ctcext_amd", "lib", "libctcext.so")
 
-def per_launch(path, counter):
+
+def per_launch(path, counter, kname):
     vals, name = [], None
     with open(path) as f:
         for row in csv.DictReader(f):
-            if "ctcx_beam_decode" in row["Kernel_Name"] and row["Counter_Name"] == counter:
+            if kname in row["Kernel_Name"] and row["Counter_Name"] == counter:
                 vals.append(float(row["Counter_Value"]))
                 name = row["Kernel_Name"]
     if not vals:
-        raise SystemExit("no ctcx_beam_decode %s rows in %s" % (counter, path))
+        raise SystemExit("no %s %s rows in %s" % (kname, counter, path))
     return sum(vals) / len(vals), len(vals), name
 
 
 def main():
-    fetch, nf, name = per_launch(sys.argv[1], "FETCH_SIZE")
-    write, nw, _ = per_launch(sys.argv[2], "WRITE_SIZE")
-    cfg = sys.argv[3] if len(sys.argv) > 3 else "cfg3"
-    rd = fetch * 1024 * 2
-    wr = write * 1024
+    fetch_csv, write_csv, cfg, seq_len, cf_csv, cw_csv, calib_json = sys.argv[1:8]
+    known = json.load(open(calib_json))
+    fetch, nf, name = per_launch(fetch_csv, "FETCH_SIZE", "ctcx_beam_decode")
+    write, nw, _ = per_launch(write_csv, "WRITE_SIZE", "ctcx_beam_decode")
+    c_rows, _, _ = per_launch(cf_csv, "FETCH_SIZE", "calib_rows")
+    c_s16, _, _ = per_launch(cf_csv, "FETCH_SIZE", "calib_stream16")
+    c_rec, _, _ = per_launch(cw_csv, "WRITE_SIZE", "calib_rec_store")
+    f_rows = known["calib_rows"] / (c_rows * 1024)
+    f_s16 = known["calib_stream16"] / (c_s16 * 1024)
+    f_rec = known["calib_rec_store_write"] / (c_rec * 1024)
+    rd = fetch * 1024 * f_rows
+    wr = write * 1024 * f_rec
+    with open(LIB, "rb") as f:
+        sha = hashlib.sha256(f.read()).hexdigest()[:16]
     out = {
-        "config": cfg, "kernel": name, "round": 1,
-        "fetch_size_kb_raw": fetch, "write_size_kb": write, "launches": [nf, nw],
+        "config": cfg, "seq_len": int(seq_len), "kernel": name, "lib_sha16": sha,
+        "fetch_size_kb_raw": fetch, "write_size_kb_raw": write, "launches": [nf, nw],
+        "calibration": {"fetch_factor_rows_4B_lane": f_rows, "fetch_factor_stream_16B_lane": f_s16,
+                        "write_factor_records_8B_lane": f_rec, "tool": "tools/fetch_calib.hip"},
         "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
         "hbm_bytes_per_launch": rd + wr,
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
-                  "'python3 bench.py --steps 2 --warmup 1 --no-cpu' (MI355X); KB -> bytes; FETCH_SIZE "
-                  "doubled per MI355X_MICROARCH.md (gfx950 tallies 128-B read requests at 64 B); WRITE_SIZE as read",
-        "note": "writes are the per-(item, frame, beam) 8-byte back-pointer records (256*1500*128*8 B = 393 MB) "
-                "that the traceback kernel walks; reads are the logit rows and row normalisers",
+                  "'python3 bench.py --config %s --steps 2 --warmup 1 --no-cpu' (MI355X); KB -> bytes; "
+                  "each counter scaled by the factor tools/fetch_calib.hip measured for the same access "
+                  "pattern over a known byte count in the same pass" % cfg,
     }
     print(json.dumps(out, indent=1))
 
