@@ -186,6 +186,7 @@ struct Ctx {
   CTCX_LDS T* est[2]; CTCX_LDS T* eest;
   const T* sctab;      // the scorer's table (global memory)
   int W, C, blank, enc, hts, wcap;
+  int hdum;            // he index of lane 0's dummy store slot
 };
 
 // Per-64-label block maxima of the logit row, right after the row (large C).
@@ -269,8 +270,12 @@ __host__ __device__ void carve(Ctx<T>& cx, CTCX_LDS char* base, int Wcap, int W,
   p += a16(4 * (size_t)cx.hts);
   cx.bloom = (CTCX_LDS uint64_t*)p;
   p += a16(8 * (size_t)Wcap);
+  // TopN elements: positions [0, max(Wcap, 128)] (the mask-form sift reads
+  // child positions up to 128, +inf sentinels past the heap), then one dummy
+  // store slot per lane
   cx.he = (CTCX_LDS HE<T>*)p;
-  p += ((size_t)Wcap + 2 + 64) * sizeof(HE<T>);
+  cx.hdum = (Wcap > 128 ? Wcap : 128) + 2;
+  p += ((size_t)cx.hdum + 64) * sizeof(HE<T>);
   cx.est[0] = cx.est[1] = cx.eest = nullptr;
   if (scored) {
     cx.est[0] = (CTCX_LDS T*)p; cx.est[1] = cx.est[0] + Wcap; cx.eest = cx.est[1] + Wcap;
@@ -682,6 +687,88 @@ __device__ __forceinline__ void wave_push_heap_v(CTCX_LDS HE<T>* he, const HeapG
   fs = keep ? vs : s0;
 }
 
+// ---------------------------------------------------------------------------
+// The same sift for heaps of up to 128 elements (one node with children per
+// lane), written as lane-mask algebra: every per-node predicate is a 64-bit
+// mask in SGPRs (a ballot), combined on the scalar unit and turned back into a
+// per-lane select by inverse_ballot, which the compiler lowers to a
+// v_cndmask on the mask itself.  One wave issues one instruction per ~4
+// cycles, and the mask form needs about half the instructions of the
+// bool-per-lane form above, with the same decisions.
+//
+// No per-length geometry: every position at or past the heap's length holds
+// a +inf sentinel (heap_sentinels; pop_heap sets each vacated position), so
+//   * a node without a right child never picks it (+inf > left),
+//   * a lane whose node has no children sees a min child of +inf: on the
+//     min-child path it is a leaf, the stop, and v lands on it -- exactly where
+//     __adjust_heap's hole would end;
+// and the only leaves that are not lanes are the children of nodes 31..63
+// (positions >= 64), a constant mask.
+// Lane `lane` of `old` takes the uniform `val` (a v_writelane; this toolchain
+// has no builtin for it, and an asm one would need M0 on gfx950's constant
+// bus): one scalar shift and one v_cndmask on the resulting lane mask.
+__device__ __forceinline__ int writelane(int old, int val, int lane) {
+  return __builtin_amdgcn_inverse_ballot_w64(1ull << lane) ? val : old;
+}
+
+__device__ __forceinline__ uint64_t lowmask(int n) { return n >= 64 ? ~0ull : ((1ull << n) - 1ull); }
+
+struct HeapM {
+  unsigned anc, req;        // ancestor bits of node j and the directions toward it
+  int aj, al, ar, dum;      // he indices: node j, its left and right child, this lane's dummy slot
+};
+
+__device__ __forceinline__ HeapM heap_m(int dum_base) {
+  HeapM g;
+  const unsigned j = threadIdx.x;
+  anc_bits(j + 1u, g.anc, g.req);
+  g.aj = (int)j + 1;
+  g.al = 2 * (int)j + 2;
+  g.ar = 2 * (int)j + 3;
+  g.dum = dum_base + (int)j;
+  return g;
+}
+
+// +inf at positions [from, 128] (he[from + 1 .. 129]: every child position a
+// lane can read)
+template <typename T>
+__device__ __forceinline__ void heap_sentinels(CTCX_LDS HE<T>* he, int from) {
+  for (int q = from + (int)threadIdx.x; q <= 128; q += 64) he_st(he, q + 1, HE<T>{pinf<T>(), -1});
+}
+
+template <typename T>
+__device__ __forceinline__ void pairs_m(const CTCX_LDS HE<T>* he, const HeapM& g, HE<T>& L, HE<T>& R) {
+  he_ld2(he, g.al, L, R);
+}
+
+// __adjust_heap(0, len, v) for len in [2, 128] with the sentinels in place:
+// stores the moves; returns the old root's min child (c0, s0) and whether v
+// stayed at the root (keep: the new root is then v, else c0).
+template <typename T>
+__device__ __forceinline__ void push_m(CTCX_LDS HE<T>* he, const HeapM& g, T vv, int vs, HE<T> L, HE<T> R,
+                                       T& c0, int& s0, bool& keep) {
+  const uint64_t pickR = __ballot(!(R.v > L.v));   // min child on the right (ties: right)
+  const bool pr = __builtin_amdgcn_inverse_ballot_w64(pickR);
+  const T cv = pr ? R.v : L.v;
+  const int cs = pr ? R.s : L.s;
+  // on the root's min-child path: every ancestor's min child points here
+  const uint64_t onp = __ballot((((unsigned)pickR ^ g.req) & g.anc) == 0u);
+  const uint64_t gt = __ballot(cv > vv);
+  // stop: min child > v, or the min child is a leaf that is not a lane
+  // (children of nodes >= 32; node 31's right child)
+  const uint64_t cnd = gt | 0xffffffff00000000ull | (pickR & 0x80000000ull);
+  const uint64_t cm = onp & cnd;
+  const uint64_t live = onp & ~__ballot((((unsigned)cm) & g.anc) != 0u);   // at or above the stop
+  const bool up = __builtin_amdgcn_inverse_ballot_w64(live & ~gt);   // takes its min child
+  const bool isk = __builtin_amdgcn_inverse_ballot_w64(live & cnd);  // the stop: v lands here or in its min child
+  const bool vg = __builtin_amdgcn_inverse_ballot_w64(gt);
+  he_st(he, up ? g.aj : g.dum, HE<T>{cv, cs});
+  he_st(he, isk ? (vg ? g.aj : (pr ? g.ar : g.al)) : g.dum, HE<T>{vv, vs});
+  c0 = uni(cv);
+  s0 = uni(cs);
+  keep = (gt & 1ull) != 0ull;
+}
+
 // peek_bottom() in the UNORDERED state: the first minimum moves to the front.
 // Returns the new front.
 template <typename T>
@@ -973,13 +1060,99 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     int nev = 0;
     uint64_t done = 0;
     while (true) {
+      if (RN == 1 && st == kTopHeap && W >= 2) {
+        // HEAP_SORTED, beams up to 128 (the mask form of the loop below, same
+        // decisions): new-child lanes wanting in (NC: live, not a branch) are
+        // accepted while they beat the front, re-offers of evicted branch
+        // children (RB) are decided one by one.  The next push's child pairs
+        // are loaded right after the previous push's stores, so their latency
+        // overlaps the selection.
+        // NC: live lanes offering a new child; LB: live lanes re-offering a
+        // branch child; RB: those of LB whose branch has been evicted (wanted
+        // whatever their score).  HEAP_SORTED is the last TopN state of the
+        // frame, so live / cev are not needed after this loop.
+        const uint64_t liveM = __ballot(live);
+        uint64_t NC = liveM & ~isbm, LB = liveM & isbm, RB = LB & __ballot(cev);
+        const HeapM geo = heap_m(cx.hdum);
+        T fv = front.v;
+        int fs = front.s;
+        int nfree = nextfree;
+        int nv = uni(nev);
+        for (;;) {
+          // the push's child pairs first: they depend only on the previous
+          // push's stores, and their latency overlaps the selection below
+          HE<T> pL, pR;
+          pairs_m(he, geo, pL, pR);
+          const uint64_t gtM = __ballot(s > fv);
+          const uint64_t m = ((gtM & NC) | RB) & ~done;
+          if (m == 0) break;
+          const int k = (int)__builtin_ctzll(m);
+          int slot;
+          if (__builtin_expect((LB >> k) & 1ull, 0)) {
+            // a re-offered branch child.  Only a re-offer can make a closed turn
+            // visible (a closed branch's new children score <= its total <=
+            // bottom): was k's turn skipped?
+            if ((__ballot(!(bt > bat)) >> k) & 1ull) {
+              const uint64_t keepM = lowmask(bcast(sl, k));   // that branch and every later one
+              NC &= keepM; LB &= keepM; RB &= keepM;
+              stop = true;
+              continue;
+            }
+            done = m ^ (m - 1ull);
+            slot = bcast(c, k);
+            if (!((gtM >> k) & 1ull)) {
+              // re-offered evicted branch rejected -> deactivated (decoder.h:200-205)
+              evr = writelane(evr, slot | kDeactRec, nv);
+              nv += 1;
+              const uint64_t dm = ~__ballot(i == slot);
+              NC &= dm; LB &= dm; RB &= dm;
+              continue;
+            }
+            // accepted: the branch's entry keeps its slot
+            if (fs < nb) {
+              evr = writelane(evr, fs, nv);
+              nv += 1;
+              RB |= LB & __ballot(c == fs);
+            }
+          } else {
+            // a new child: it takes the evicted front's slot, or a fresh one when
+            // the front is a branch's entry (which is reset and flagged instead)
+            done = m ^ (m - 1ull);   // lanes <= k
+            slot = fs;
+            if (fs < nb) {
+              slot = nfree;
+              nfree += 1;
+              evr = writelane(evr, fs, nv);
+              nv += 1;
+              RB |= LB & __ballot(c == fs);
+            }
+          }
+          slot = uni(slot);
+          const T k_s = bcast(s, k);
+          myslot = (myslot == fs) ? -1 : myslot;
+          myslot = __builtin_amdgcn_inverse_ballot_w64(1ull << k) ? slot : myslot;
+          T c0;
+          int s0;
+          bool keep;
+          push_m<T>(he, geo, k_s, slot, pL, pR, c0, s0, keep);   // push = pop_heap(W + 1)
+          fv = uni(keep ? k_s : c0);
+          fs = uni(keep ? slot : s0);
+          bat = (sl > k) ? fv : bat;
+        }
+        nev = nv;
+        front.v = fv;
+        front.s = fs;
+        bottom = fv;
+        nextfree = nfree;
+        break;
+      }
       if (st == kTopHeap) {
         // HEAP_SORTED (the beam is full): every wanted new child is accepted
         // and replaces the front; a re-offered evicted branch is accepted iff
         // it beats the bottom.  Per-lane flags are kept as wave masks so one
         // compare per event feeds both decisions.
         uint64_t liveM = __ballot(live), cevM = __ballot(cev);
-        const HeapGeo<RN> geo = heap_geo<RN>(W, cx.wcap + 2);
+        const HeapGeo<RN> geo = heap_geo<RN>(W, cx.hdum);
         // the front and the bump pointer as (uniform) VGPR values: nothing on
         // the event chain below leaves the vector unit except the event pick
         T fv = front.v;
@@ -1091,8 +1264,9 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
 #endif
             wave_make_heap(he, W + 1);
             const HE<T> r0 = he_ld(he, 1);
-            front = wave_adjust_heap<T, RN>(he, heap_geo<RN>(W, cx.wcap + 2), nv, W);   // pop_heap(W + 1)
+            front = wave_adjust_heap<T, RN>(he, heap_geo<RN>(W, cx.hdum), nv, W);   // pop_heap(W + 1)
             if (lane == 0) he_st(he, W + 1, r0);
+            if (RN == 1 && W >= 2) heap_sentinels(he, W);   // the mask-form sift's geometry
             st = kTopHeap;
 #ifdef CTCX_FASTLOOP_PROF
             if (pc) pc[14] += __builtin_amdgcn_s_memtime() - q4;
@@ -1164,12 +1338,40 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
   }
   // Extract() of the next frame (decoder.h:84): sort_heap, or std::sort
   int nout;
-  if (st == kTopHeap) {
+  if (RN == 1 && st == kTopHeap && W >= 2) {
+    // sort_heap in mask form (beams up to 128).  pop_heap(len) parks the old
+    // front at position len - 1, which no later sift reads: the slot goes
+    // straight into a register lane (position p: lane p of srt[p >> 6])
+    // instead of back to LDS.
+    const HeapM geo = heap_m(cx.hdum);
+    int fs = front.s;
+    int srt0 = 0, srt1 = 0;
+    for (int len = W; len > 2; --len) {
+      const HE<T> v = he_ld(he, len);   // e[len-1] (uniform address)
+      if (lane == 0) he_st(he, len, HE<T>{pinf<T>(), -1});   // vacated: a sentinel for the sift over len - 1
+      HE<T> pL, pR;
+      pairs_m(he, geo, pL, pR);
+      const int pos = len - 1;
+      if (pos >= 64) srt1 = writelane(srt1, fs, pos - 64);
+      else srt0 = writelane(srt0, fs, pos);
+      T c0;
+      int s0;
+      bool keep;
+      push_m<T>(he, geo, v.v, v.s, pL, pR, c0, s0, keep);
+      fs = keep ? uni(v.s) : s0;
+    }
+    // pop_heap(2): the front goes to position 1, e[1] becomes the root
+    srt0 = writelane(srt0, fs, 1);
+    srt0 = writelane(srt0, uni(he_ld(he, 2).s), 0);
+    nout = W;
+    if (lane < nout) cx.sorted[lane] = srt0;
+    if (lane + 64 < nout) cx.sorted[lane + 64] = srt1;
+  } else if (st == kTopHeap) {
     // pop_heap(len): e[len-1] <- e[0], then sift the old e[len-1] from the root
     T fv = front.v;
     int fs = front.s;
     for (int len = W; len > 1; --len) {
-      const HeapGeo<RN> geo = heap_geo<RN>(len - 1, cx.wcap + 2);
+      const HeapGeo<RN> geo = heap_geo<RN>(len - 1, cx.hdum);
       const HE<T> v = he_ld(he, len);   // e[len-1], read before the old front lands there
       HeapPairs<T, RN> hp;
       heap_pairs<T, RN>(he, geo, hp);
