@@ -769,6 +769,136 @@ __device__ __forceinline__ void push_m(CTCX_LDS HE<T>* he, const HeapM& g, T vv,
   keep = (gt & 1ull) != 0ull;
 }
 
+// The HEAP_SORTED event loop for float beams of up to 128 (exact_step), as one
+// hand-scheduled asm block: the same selections, bookkeeping and push_m sift as
+// the C++ loop it replaces (the stop found by s_ff1 of the path nodes meeting
+// the stop condition: path nodes are ancestors of one another, so the
+// shallowest is the lowest lane), in ~50 instructions per accepted offer (the
+// compiled loop took ~85, with the uniform state spilled into VGPR lanes).  It
+// runs until no live lane wants in (returns 0) or the next wanted lane k
+// re-offers a branch child (returns 1: the caller decides that event).  It is
+// software-pipelined: as soon as a push has its new front, the next event's
+// selection starts, interleaved with the rest of the push (stop, moves,
+// stores); the next push's child pairs are read right after the stores.
+//   state (SGPR): NC / RB / done lane masks, the front (fv, fs), the bump
+//   pointer, the eviction-record count; (VGPR): myslot, evr, bat.
+//   he addresses are LDS byte addresses: node j (aj), its child pair (al, ar),
+//   the lane's dummy slot (dum).
+// Hazards: every VALU-written SGPR is read by a VALU two or more instructions
+// later (or behind an s_nop); DS operand registers are rewritten only after
+// the s_waitcnt lgkmcnt(0) that retires their instruction; lane selects come
+// from SALU.  Temporaries: s84..s99, vcc, v232..v243 (clobbered).
+#ifdef CTCX_PHASES
+#define CTCX_EVCNT "s_add_u32 %[cnt], %[cnt], 1\n\t"   // diagnostics builds: count the pushes
+#else
+#define CTCX_EVCNT ""
+#endif
+__device__ __forceinline__ int heap_events_f32(float s, int c, int sl, unsigned anc, unsigned req, unsigned aj,
+                                               unsigned al, unsigned ar, unsigned dum, int& myslot, int& evr,
+                                               float& bat, uint64_t& NC, uint64_t& RB, uint64_t& done, uint64_t LB,
+                                               float& fv, int& fs, int& nfree, int& nv, int nb, int& k, int& cnt) {
+  int st;
+  const uint64_t k31 = 0x80000000ull, khi = 0xffffffff00000000ull;
+  asm volatile(
+      "s_mov_b32 %[st], 0\n\t"
+      // select the first event
+      "v_cmp_lt_f32_e64 s[88:89], %[fv], %[s]\n\t"          // s > front
+      "s_and_b64 s[88:89], s[88:89], %[nc]\n\t"
+      "s_or_b64 s[88:89], s[88:89], %[rb]\n\t"
+      "s_andn2_b64 s[88:89], s[88:89], %[done]\n\t"        // m (SCC: m != 0)
+      "s_cbranch_scc0 .Lev_exit_%=\n\t"
+      "s_ff1_i32_b64 %[k], s[88:89]\n\t"
+      "s_bitcmp1_b64 %[lb], %[k]\n\t"
+      "s_cbranch_scc1 .Lev_rare_%=\n\t"
+      "ds_read_b128 v[232:235], %[al]\n\t"                 // its child pairs (L.v, L.s, R.v, R.s)
+      "s_branch .Lev_tail_%=\n"
+      // push of event k (v = s84, slot = s85), then the next selection
+      // interleaved with the push's second half
+      ".Lev_loop_%=:\n\t"
+      CTCX_EVCNT
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "v_cmp_ngt_f32_e64 s[92:93], v234, v232\n\t"         // pickR = !(R > L)
+      "v_mov_b32_e32 v240, s84\n\t"
+      "v_mov_b32_e32 v241, s85\n\t"
+      "v_cndmask_b32_e64 v237, v232, v234, s[92:93]\n\t"   // cv
+      "v_cndmask_b32_e64 v238, v233, v235, s[92:93]\n\t"   // cs
+      "v_xor_b32_e32 v239, s92, %[req]\n\t"
+      "v_cmp_lt_f32_e64 s[96:97], s84, v237\n\t"           // gt: min child > v
+      "v_and_b32_e32 v239, v239, %[anc]\n\t"
+      "v_readfirstlane_b32 s86, v237\n\t"                  // c0: the root's min child
+      "v_cmp_eq_u32_e64 s[94:95], 0, v239\n\t"             // onp: on the root's min-child path
+      "v_readfirstlane_b32 s87, v238\n\t"
+      "s_and_b64 s[98:99], s[92:93], %[k31]\n\t"
+      "s_or_b64 s[98:99], s[98:99], %[khi]\n\t"
+      "s_bitcmp1_b32 s96, 0\n\t"                           // keep: v stays at the root
+      "s_cselect_b32 %[fv], s84, s86\n\t"                  // the new front
+      "s_cselect_b32 %[fs], s85, s87\n\t"
+      "s_or_b64 s[98:99], s[98:99], s[96:97]\n\t"          // cnd: gt, or the min child is a non-lane leaf
+      "v_cmp_lt_i32_e64 vcc, %[k], %[sl]\n\t"              // turns starting after lane k see the new bottom
+      "v_cmp_lt_f32_e64 s[88:89], %[fv], %[s]\n\t"         // next: s > front
+      "s_and_b64 s[90:91], s[94:95], s[98:99]\n\t"         // cm (path nodes meeting the stop condition)
+      "s_ff1_i32_b64 s86, s[90:91]\n\t"                    // the stop: the shallowest of them
+      "v_mov_b32_e32 v242, %[fv]\n\t"
+      "s_lshl_b64 s[90:91], -2, s86\n\t"
+      "s_andn2_b64 s[94:95], s[94:95], s[90:91]\n\t"       // live: path nodes at or above the stop
+      "s_andn2_b64 s[90:91], s[94:95], s[96:97]\n\t"       // up: takes its min child
+      "s_lshl_b64 s[94:95], 1, s86\n\t"                    // the stop
+      "v_cndmask_b32_e32 %[bat], %[bat], v242, vcc\n\t"
+      "v_cndmask_b32_e64 v236, %[al], %[ar], s[92:93]\n\t"
+      "v_cndmask_b32_e64 v239, %[dum], %[aj], s[90:91]\n\t"
+      "v_cndmask_b32_e64 v236, v236, %[aj], s[96:97]\n\t"  // v lands on the stop (gt) or its min child
+      "ds_write2_b32 v239, v237, v238 offset1:1\n\t"
+      "v_cndmask_b32_e64 v236, %[dum], v236, s[94:95]\n\t"
+      "s_and_b64 s[88:89], s[88:89], %[nc]\n\t"
+      "s_or_b64 s[88:89], s[88:89], %[rb]\n\t"
+      "ds_write2_b32 v236, v240, v241 offset1:1\n\t"
+      "ds_read_b128 v[232:235], %[al]\n\t"                 // the next push's child pairs
+      "s_andn2_b64 s[88:89], s[88:89], %[done]\n\t"        // next m
+      "s_cbranch_scc0 .Lev_exit_%=\n\t"
+      "s_ff1_i32_b64 %[k], s[88:89]\n\t"
+      "s_bitcmp1_b64 %[lb], %[k]\n\t"
+      "s_cbranch_scc1 .Lev_rare_%=\n"
+      ".Lev_tail_%=:\n\t"
+      "s_lshl_b64 s[90:91], -2, %[k]\n\t"
+      "s_not_b64 %[done], s[90:91]\n\t"                    // done = lanes <= k
+      "v_readlane_b32 s84, %[s], %[k]\n\t"                 // v = offer k's score
+      "s_mov_b32 s85, %[fs]\n\t"                           // slot = the front's
+      "s_cmp_lt_i32 %[fs], %[nb]\n\t"
+      "s_cbranch_scc1 .Lev_evb_%=\n"
+      ".Lev_slot_%=:\n\t"
+      "v_cmp_eq_u32_e64 s[90:91], %[fs], %[my]\n\t"        // an entry accepted in this chunk is the evicted front
+      "s_lshl_b64 vcc, 1, %[k]\n\t"
+      "v_mov_b32_e32 v243, s85\n\t"
+      "v_cndmask_b32_e64 %[my], %[my], -1, s[90:91]\n\t"
+      "v_cndmask_b32_e32 %[my], %[my], v243, vcc\n\t"      // lane k: its entry's slot
+      "s_branch .Lev_loop_%=\n"
+      // the evicted front is a branch's entry: a fresh slot; record the
+      // eviction; a live re-offer of that branch is now wanted
+      ".Lev_evb_%=:\n\t"
+      "s_mov_b32 s85, %[nfree]\n\t"
+      "s_add_u32 %[nfree], %[nfree], 1\n\t"
+      "s_lshl_b64 s[90:91], 1, %[nv]\n\t"
+      "v_mov_b32_e32 v243, %[fs]\n\t"
+      "s_add_u32 %[nv], %[nv], 1\n\t"
+      "v_cndmask_b32_e64 %[evr], %[evr], v243, s[90:91]\n\t"
+      "v_cmp_eq_u32_e64 s[90:91], %[fs], %[c]\n\t"
+      "s_and_b64 s[90:91], s[90:91], %[lb]\n\t"
+      "s_or_b64 %[rb], %[rb], s[90:91]\n\t"
+      "s_branch .Lev_slot_%=\n"
+      ".Lev_rare_%=:\n\t"
+      "s_mov_b32 %[st], 1\n"
+      ".Lev_exit_%=:\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : [my] "+v"(myslot), [evr] "+v"(evr), [bat] "+v"(bat), [nc] "+s"(NC), [rb] "+s"(RB), [done] "+s"(done),
+        [fv] "+s"(fv), [fs] "+s"(fs), [nfree] "+s"(nfree), [nv] "+s"(nv), [k] "=&s"(k), [st] "=&s"(st), [cnt] "+s"(cnt)
+      : [s] "v"(s), [c] "v"(c), [sl] "v"(sl), [anc] "v"(anc), [req] "v"(req), [aj] "v"(aj), [al] "v"(al),
+        [ar] "v"(ar), [dum] "v"(dum), [lb] "s"(LB), [nb] "s"(nb), [k31] "s"(k31), [khi] "s"(khi)
+      : "memory", "vcc", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96",
+        "s97", "s98", "s99", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239", "v240", "v241",
+        "v242", "v243");
+  return st;
+}
+
 // peek_bottom() in the UNORDERED state: the first minimum moves to the front.
 // Returns the new front.
 template <typename T>
@@ -1078,20 +1208,27 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
         int fs = front.s;
         int nfree = nextfree;
         int nv = uni(nev);
-        for (;;) {
-          // the push's child pairs first: they depend only on the previous
-          // push's stores, and their latency overlaps the selection below
-          HE<T> pL, pR;
-          pairs_m(he, geo, pL, pR);
-          const uint64_t gtM = __ballot(s > fv);
-          const uint64_t m = ((gtM & NC) | RB) & ~done;
-          if (m == 0) break;
-          const int k = (int)__builtin_ctzll(m);
-          int slot;
-          if (__builtin_expect((LB >> k) & 1ull, 0)) {
-            // a re-offered branch child.  Only a re-offer can make a closed turn
-            // visible (a closed branch's new children score <= its total <=
+        if constexpr (sizeof(T) == 4) {
+          // float: the hand-scheduled loop; re-offers of branch children come
+          // back here one at a time
+          const unsigned heb = (unsigned)(uintptr_t)he;   // LDS byte address of he[0]
+          const unsigned aj = heb + 8u * (unsigned)(lane + 1), al = heb + 8u * (unsigned)(2 * lane + 2);
+          const unsigned ar = al + 8u, dum = heb + 8u * (unsigned)(cx.hdum + lane);
+          for (;;) {
+            int k;
+            fv = uni(fv); fs = uni(fs); nfree = uni(nfree); nv = uni(nv);
+            int nev_asm = 0;
+            const uint64_t ta = pc ? __builtin_amdgcn_s_memtime() : 0;
+            const int est = heap_events_f32(s, c, sl, geo.anc, geo.req, aj, al, ar, dum, myslot, evr, bat, NC, RB, done,
+                                            LB, fv, fs, nfree, nv, nb, k, nev_asm);
+            if (pc) { pc[13] += __builtin_amdgcn_s_memtime() - ta; pc[6] += uni(nev_asm); pc[12] += 1; }
+            if (est == 0) break;
+            k = uni(k);
+            // lane k re-offers a branch child.  Only a re-offer can make a closed
+            // turn visible (a closed branch's new children score <= its total <=
             // bottom): was k's turn skipped?
+            const uint64_t gtM = __ballot(s > fv);
+            const uint64_t m = ((gtM & NC) | RB) & ~done;   // its lowest lane is k
             if ((__ballot(!(bt > bat)) >> k) & 1ull) {
               const uint64_t keepM = lowmask(bcast(sl, k));   // that branch and every later one
               NC &= keepM; LB &= keepM; RB &= keepM;
@@ -1099,12 +1236,12 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
               continue;
             }
             done = m ^ (m - 1ull);
-            slot = bcast(c, k);
+            const int kc = bcast(c, k);
             if (!((gtM >> k) & 1ull)) {
               // re-offered evicted branch rejected -> deactivated (decoder.h:200-205)
-              evr = writelane(evr, slot | kDeactRec, nv);
+              evr = writelane(evr, kc | kDeactRec, nv);
               nv += 1;
-              const uint64_t dm = ~__ballot(i == slot);
+              const uint64_t dm = ~__ballot(i == kc);
               NC &= dm; LB &= dm; RB &= dm;
               continue;
             }
@@ -1114,30 +1251,81 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
               nv += 1;
               RB |= LB & __ballot(c == fs);
             }
-          } else {
-            // a new child: it takes the evicted front's slot, or a fresh one when
-            // the front is a branch's entry (which is reset and flagged instead)
-            done = m ^ (m - 1ull);   // lanes <= k
-            slot = fs;
-            if (fs < nb) {
-              slot = nfree;
-              nfree += 1;
-              evr = writelane(evr, fs, nv);
-              nv += 1;
-              RB |= LB & __ballot(c == fs);
-            }
+            const T k_s = bcast(s, k);
+            myslot = (myslot == fs) ? -1 : myslot;
+            myslot = __builtin_amdgcn_inverse_ballot_w64(1ull << k) ? kc : myslot;
+            HE<T> pL, pR;
+            pairs_m(he, geo, pL, pR);
+            T c0;
+            int s0;
+            bool keep;
+            push_m<T>(he, geo, k_s, kc, pL, pR, c0, s0, keep);
+            fv = keep ? k_s : c0;
+            fs = keep ? kc : s0;
+            bat = (sl > k) ? fv : bat;
           }
-          slot = uni(slot);
-          const T k_s = bcast(s, k);
-          myslot = (myslot == fs) ? -1 : myslot;
-          myslot = __builtin_amdgcn_inverse_ballot_w64(1ull << k) ? slot : myslot;
-          T c0;
-          int s0;
-          bool keep;
-          push_m<T>(he, geo, k_s, slot, pL, pR, c0, s0, keep);   // push = pop_heap(W + 1)
-          fv = uni(keep ? k_s : c0);
-          fs = uni(keep ? slot : s0);
-          bat = (sl > k) ? fv : bat;
+        } else {
+          for (;;) {
+            // the push's child pairs first: they depend only on the previous
+            // push's stores, and their latency overlaps the selection below
+            HE<T> pL, pR;
+            pairs_m(he, geo, pL, pR);
+            const uint64_t gtM = __ballot(s > fv);
+            const uint64_t m = ((gtM & NC) | RB) & ~done;
+            if (m == 0) break;
+            const int k = (int)__builtin_ctzll(m);
+            int slot;
+            if (__builtin_expect((LB >> k) & 1ull, 0)) {
+              // a re-offered branch child.  Only a re-offer can make a closed turn
+              // visible (a closed branch's new children score <= its total <=
+              // bottom): was k's turn skipped?
+              if ((__ballot(!(bt > bat)) >> k) & 1ull) {
+                const uint64_t keepM = lowmask(bcast(sl, k));   // that branch and every later one
+                NC &= keepM; LB &= keepM; RB &= keepM;
+                stop = true;
+                continue;
+              }
+              done = m ^ (m - 1ull);
+              slot = bcast(c, k);
+              if (!((gtM >> k) & 1ull)) {
+                // re-offered evicted branch rejected -> deactivated (decoder.h:200-205)
+                evr = writelane(evr, slot | kDeactRec, nv);
+                nv += 1;
+                const uint64_t dm = ~__ballot(i == slot);
+                NC &= dm; LB &= dm; RB &= dm;
+                continue;
+              }
+              // accepted: the branch's entry keeps its slot
+              if (fs < nb) {
+                evr = writelane(evr, fs, nv);
+                nv += 1;
+                RB |= LB & __ballot(c == fs);
+              }
+            } else {
+              // a new child: it takes the evicted front's slot, or a fresh one when
+              // the front is a branch's entry (which is reset and flagged instead)
+              done = m ^ (m - 1ull);   // lanes <= k
+              slot = fs;
+              if (fs < nb) {
+                slot = nfree;
+                nfree += 1;
+                evr = writelane(evr, fs, nv);
+                nv += 1;
+                RB |= LB & __ballot(c == fs);
+              }
+            }
+            slot = uni(slot);
+            const T k_s = bcast(s, k);
+            myslot = (myslot == fs) ? -1 : myslot;
+            myslot = __builtin_amdgcn_inverse_ballot_w64(1ull << k) ? slot : myslot;
+            T c0;
+            int s0;
+            bool keep;
+            push_m<T>(he, geo, k_s, slot, pL, pR, c0, s0, keep);   // push = pop_heap(W + 1)
+            fv = uni(keep ? k_s : c0);
+            fs = uni(keep ? slot : s0);
+            bat = (sl > k) ? fv : bat;
+          }
         }
         nev = nv;
         front.v = fv;

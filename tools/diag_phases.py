@@ -22,10 +22,12 @@ d.lib.ctcext_phase_counters(d.handle, ctypes.c_void_p(buf.ctypes.data), B * 16)
 m = buf.astype(np.float64).mean(0)
 fr = m[7]
 names = ["rowload", "recursion", "grow", "extract", "commit", "literal", "heap events", "frames",
-         "scoring", "eventloop", "ev:select", "chunks", "ev:bookkeep", "ev:heapop", "makeheap", "flush"]
-CYC = {0, 1, 2, 3, 4, 5, 8, 9, 10, 12, 13, 14, 15}
+         "scoring", "eventloop", "ev:select", "chunks", "asm calls", "asm loop", "makeheap", "flush"]
+CYC = {0, 1, 2, 3, 4, 5, 8, 9, 10, 13, 14, 15}
 print("B=%d T=%d W=%d P=%d C=%d decode_ms=%.1f" % (B, T, W, P, C, d.last_stats["decode_kernel_ms"]))
 for k in range(16):
     if k == 7:
         continue
     print("  %-10s %12.0f %s/frame" % (names[k], m[k] / fr, "cycles" if k in CYC else "count"))
+if m[6] > 0:
+    print("  asm loop cycles per push (incl. entry/exit): %.0f" % (m[13] / m[6]))

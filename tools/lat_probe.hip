@@ -80,18 +80,41 @@ __global__ void probe(int n, float* out, int seed) {
   t1 = __builtin_amdgcn_s_memtime();
   acc += w;
   if (lane == 0) out[6] = (float)(t1 - t0) / n;
+  // 8: ds_bpermute chain (gather from lane 2j+1, the heap child pattern)
+  int g = lane;
+  t0 = __builtin_amdgcn_s_memtime();
+  for (int k = 0; k < n; ++k) g = __builtin_amdgcn_ds_bpermute(((2 * lane + 1 + (g & 1)) & 63) * 4, g) + 1;
+  t1 = __builtin_amdgcn_s_memtime();
+  acc += g;
+  if (lane == 0) out[8] = (float)(t1 - t0) / n;
+  // 9: the push pattern: two 8-byte stores (per-lane addresses) then a 16-byte read
+  typedef unsigned u2 __attribute__((ext_vector_type(2)));
+  typedef unsigned u4 __attribute__((ext_vector_type(4)));
+  unsigned hv = lane;
+  t0 = __builtin_amdgcn_s_memtime();
+  for (int k = 0; k < n; ++k) {
+    u2 a; a.x = hv; a.y = hv + 1;
+    *(LDS u2*)(b + 2 * ((lane + hv) & 127)) = a;
+    *(LDS u2*)(b + 2 * (128 + lane)) = a;
+    const u4 r = *(LDS u4*)(b + 4 * (lane & 63));
+    hv = r.x + r.w;
+  }
+  t1 = __builtin_amdgcn_s_memtime();
+  acc += hv;
+  if (lane == 0) out[9] = (float)(t1 - t0) / n;
   if (lane == 0) out[7] = acc;
 }
 
 int main() {
   float* o;
-  (void)hipMalloc(&o, 64);
+  (void)hipMalloc(&o, 256);
   hipLaunchKernelGGL(probe, dim3(1), dim3(64), 0, 0, 1000, o, 0);
   hipLaunchKernelGGL(probe, dim3(1), dim3(64), 0, 0, 1000, o, 1);
-  float h[8];
-  (void)hipMemcpy(h, o, 32, hipMemcpyDeviceToHost);
+  float h[10];
+  (void)hipMemcpy(h, o, 40, hipMemcpyDeviceToHost);
   const char* names[] = {"lds read chain", "cmp->ballot->branch", "readfirstlane chain", "lds store->load",
-                         "ds_read_b128 -> readfirstlane", "salu/readfirstlane loop", "lane0 store + read"};
-  for (int i = 0; i < 7; ++i) printf("%-32s %7.1f cycles/iter\n", names[i], h[i]);
+                         "ds_read_b128 -> readfirstlane", "salu/readfirstlane loop", "lane0 store + read",
+                         "(acc)", "ds_bpermute chain", "2x ds_write_b64 + ds_read_b128"};
+  for (int i = 0; i < 10; ++i) if (i != 7) printf("%-32s %7.1f cycles/iter\n", names[i], h[i]);
   return 0;
 }
