@@ -899,6 +899,77 @@ __device__ __forceinline__ int heap_events_f32(float s, int c, int sl, unsigned 
   return st;
 }
 
+// sort_heap for float beams of up to 128 (exact_step's Extract), pops
+// pop_heap(len) for len = hi down to lo + 1 as one hand-scheduled asm loop:
+// the front goes to position len - 1 -- recorded as lane (len - 1 - base) of
+// srt instead of stored, no later sift reads it -- position len - 1 becomes a
+// +inf sentinel, and e[len - 1] sifts from the root over len - 1 elements
+// (the push_m sift).  Temporaries: s84..s99, v232..v251 (clobbered); DS
+// operand registers are rewritten only after the s_waitcnt that retires them.
+__device__ __forceinline__ void extract_f32(unsigned heb, int hi, int lo, int base, unsigned anc, unsigned req,
+                                            unsigned aj, unsigned al, unsigned ar, unsigned dum, int& srt, int& fs) {
+  const uint64_t k31 = 0x80000000ull, khi = 0xffffffff00000000ull;
+  asm volatile(
+      "s_mov_b32 s84, %[hi]\n\t"
+      "s_mov_b64 s[90:91], 1\n\t"                          // lane 0
+      "v_mov_b32_e32 v242, 0x7f800000\n\t"                 // the sentinel (+inf, -1)
+      "v_mov_b32_e32 v243, -1\n"
+      ".Lx_top_%=:\n\t"
+      "s_cmp_le_i32 s84, %[lo]\n\t"
+      "s_cbranch_scc1 .Lx_end_%=\n\t"
+      "s_lshl_b32 s85, s84, 3\n\t"
+      "s_add_u32 s85, s85, %[heb]\n\t"                     // he[len]: position len - 1
+      "s_sub_u32 s86, s84, 1\n\t"
+      "s_sub_u32 s86, s86, %[base]\n\t"
+      "s_lshl_b64 s[88:89], 1, s86\n\t"                    // its lane in srt
+      "v_mov_b32_e32 v236, s85\n\t"
+      "v_mov_b32_e32 v240, %[fs]\n\t"
+      "ds_read_b64 v[238:239], v236\n\t"                   // e[len - 1] (every lane: broadcast)
+      "v_cndmask_b32_e64 v241, %[dum], v236, s[90:91]\n\t"
+      "v_cndmask_b32_e64 %[srt], %[srt], v240, s[88:89]\n\t"   // the front: position len - 1
+      "ds_write_b64 v241, v[242:243]\n\t"                  // lane 0: the sentinel
+      "ds_read_b128 v[232:235], %[al]\n\t"                 // child pairs
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "v_cmp_ngt_f32_e64 s[92:93], v234, v232\n\t"         // pickR
+      "v_mov_b32_e32 v244, v238\n\t"
+      "v_mov_b32_e32 v245, v239\n\t"
+      "v_cndmask_b32_e64 v248, v232, v234, s[92:93]\n\t"   // cv
+      "v_cndmask_b32_e64 v249, v233, v235, s[92:93]\n\t"   // cs
+      "v_xor_b32_e32 v251, s92, %[req]\n\t"
+      "v_cmp_lt_f32_e64 s[96:97], v238, v248\n\t"          // gt: min child > v
+      "v_and_b32_e32 v251, v251, %[anc]\n\t"
+      "v_readfirstlane_b32 s87, v239\n\t"                  // v's slot
+      "v_cmp_eq_u32_e64 s[94:95], 0, v251\n\t"             // onp
+      "v_readfirstlane_b32 s86, v249\n\t"                  // s0
+      "s_and_b64 s[98:99], s[92:93], %[k31]\n\t"
+      "s_or_b64 s[98:99], s[98:99], %[khi]\n\t"
+      "s_or_b64 s[98:99], s[98:99], s[96:97]\n\t"          // cnd
+      "s_and_b64 s[88:89], s[94:95], s[98:99]\n\t"         // cm
+      "s_ff1_i32_b64 s88, s[88:89]\n\t"                    // the stop
+      "s_lshl_b64 s[88:89], -2, s88\n\t"
+      "s_andn2_b64 s[94:95], s[94:95], s[88:89]\n\t"       // live
+      "s_andn2_b64 s[88:89], s[94:95], s[96:97]\n\t"       // up
+      "s_and_b64 s[98:99], s[94:95], s[98:99]\n\t"         // the stop
+      "v_cndmask_b32_e64 v250, %[al], %[ar], s[92:93]\n\t"
+      "v_cndmask_b32_e64 v247, %[dum], %[aj], s[88:89]\n\t"
+      "v_cndmask_b32_e64 v250, v250, %[aj], s[96:97]\n\t"
+      "ds_write2_b32 v247, v248, v249 offset1:1\n\t"
+      "v_cndmask_b32_e64 v250, %[dum], v250, s[98:99]\n\t"
+      "s_bitcmp1_b32 s96, 0\n\t"                           // keep: v stays at the root
+      "s_cselect_b32 %[fs], s87, s86\n\t"
+      "ds_write2_b32 v250, v244, v245 offset1:1\n\t"
+      "s_sub_u32 s84, s84, 1\n\t"
+      "s_branch .Lx_top_%=\n"
+      ".Lx_end_%=:\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : [srt] "+v"(srt), [fs] "+s"(fs)
+      : [heb] "s"(heb), [hi] "s"(hi), [lo] "s"(lo), [base] "s"(base), [anc] "v"(anc), [req] "v"(req), [aj] "v"(aj),
+        [al] "v"(al), [ar] "v"(ar), [dum] "v"(dum), [k31] "s"(k31), [khi] "s"(khi)
+      : "memory", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97",
+        "s98", "s99", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239", "v240", "v241", "v242",
+        "v243", "v244", "v245", "v246", "v247", "v248", "v249", "v250", "v251");
+}
+
 // peek_bottom() in the UNORDERED state: the first minimum moves to the front.
 // Returns the new front.
 template <typename T>
@@ -1220,7 +1291,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
             int nev_asm = 0;
             const uint64_t ta = pc ? __builtin_amdgcn_s_memtime() : 0;
             const int est = heap_events_f32(s, c, sl, geo.anc, geo.req, aj, al, ar, dum, myslot, evr, bat, NC, RB, done,
-                                            LB, fv, fs, nfree, nv, nb, k, nev_asm);
+                                            LB, fv, fs, nfree, nv, uni(nb), k, nev_asm);
             if (pc) { pc[13] += __builtin_amdgcn_s_memtime() - ta; pc[6] += uni(nev_asm); pc[12] += 1; }
             if (est == 0) break;
             k = uni(k);
@@ -1534,19 +1605,29 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     const HeapM geo = heap_m(cx.hdum);
     int fs = front.s;
     int srt0 = 0, srt1 = 0;
-    for (int len = W; len > 2; --len) {
-      const HE<T> v = he_ld(he, len);   // e[len-1] (uniform address)
-      if (lane == 0) he_st(he, len, HE<T>{pinf<T>(), -1});   // vacated: a sentinel for the sift over len - 1
-      HE<T> pL, pR;
-      pairs_m(he, geo, pL, pR);
-      const int pos = len - 1;
-      if (pos >= 64) srt1 = writelane(srt1, fs, pos - 64);
-      else srt0 = writelane(srt0, fs, pos);
-      T c0;
-      int s0;
-      bool keep;
-      push_m<T>(he, geo, v.v, v.s, pL, pR, c0, s0, keep);
-      fs = keep ? uni(v.s) : s0;
+    if constexpr (sizeof(T) == 4) {
+      const unsigned heb = (unsigned)(uintptr_t)he;
+      const unsigned aj = heb + 8u * (unsigned)(lane + 1), al = heb + 8u * (unsigned)(2 * lane + 2);
+      const unsigned ar = al + 8u, dum = heb + 8u * (unsigned)(cx.hdum + lane);
+      fs = uni(fs);
+      // positions 127..64 into srt1, 63..2 into srt0
+      if (W > 64) extract_f32(heb, uni(W), 64, 64, geo.anc, geo.req, aj, al, ar, dum, srt1, fs);
+      extract_f32(heb, uni(W < 64 ? W : 64), 2, 0, geo.anc, geo.req, aj, al, ar, dum, srt0, fs);
+    } else {
+      for (int len = W; len > 2; --len) {
+        const HE<T> v = he_ld(he, len);   // e[len-1] (uniform address)
+        if (lane == 0) he_st(he, len, HE<T>{pinf<T>(), -1});   // vacated: a sentinel for the sift over len - 1
+        HE<T> pL, pR;
+        pairs_m(he, geo, pL, pR);
+        const int pos = len - 1;
+        if (pos >= 64) srt1 = writelane(srt1, fs, pos - 64);
+        else srt0 = writelane(srt0, fs, pos);
+        T c0;
+        int s0;
+        bool keep;
+        push_m<T>(he, geo, v.v, v.s, pL, pR, c0, s0, keep);
+        fs = keep ? uni(v.s) : s0;
+      }
     }
     // pop_heap(2): the front goes to position 1, e[1] becomes the root
     srt0 = writelane(srt0, fs, 1);
