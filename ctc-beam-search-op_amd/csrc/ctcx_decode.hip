@@ -1235,6 +1235,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     const int sl = lane - li;
     T bat = sl > 0 ? bottom : NI;
     const uint64_t startsM = __ballot(valid && li == 0 && lane != 0);   // branch turns starting mid-chunk
+    if (pc) pc[10] += __builtin_amdgcn_s_memtime() - tc0;
     if (full && !__ballot(live && (s > bottom || ((cx.bloom[i] >> (l & 63)) & 1ull)))) {
       if (startsM & ~__ballot(bt > bottom)) break;   // no event here: every start sees this bottom
       continue;
@@ -1548,9 +1549,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     // the turn continuing into the next chunk: skipped -> so is every later one
     if (full && (__ballot(valid && !(bt > bat)) >> 63) & 1ull) stop = true;
     // flush: resets and flags first, then the surviving accepted entries
-#ifdef CTCX_FASTLOOP_PROF
-    const uint64_t q5 = __builtin_amdgcn_s_memtime();
-#endif
+    const uint64_t q5 = pc ? __builtin_amdgcn_s_memtime() : 0;
     if (lane < nev) {
       const int rs = evr & ~kDeactRec;
       if (evr & kDeactRec) {
@@ -1573,9 +1572,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       if constexpr (SC::kStateful) cx.eest[myslot] = cst;
       if (isbc) __hip_atomic_fetch_and(&cx.bst[c], ~S_EVICT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-#ifdef CTCX_FASTLOOP_PROF
     if (pc) pc[15] += __builtin_amdgcn_s_memtime() - q5;
-#endif
     if (pc) pc[9] += __builtin_amdgcn_s_memtime() - tc1;
   }
 

@@ -22,7 +22,7 @@ d.lib.ctcext_phase_counters(d.handle, ctypes.c_void_p(buf.ctypes.data), B * 16)
 m = buf.astype(np.float64).mean(0)
 fr = m[7]
 names = ["rowload", "recursion", "grow", "extract", "commit", "literal", "heap events", "frames",
-         "scoring", "eventloop", "ev:select", "chunks", "asm calls", "asm loop", "makeheap", "flush"]
+         "scoring", "eventloop", "score:pre-skip", "chunks", "asm calls", "asm loop", "makeheap", "flush"]
 CYC = {0, 1, 2, 3, 4, 5, 8, 9, 10, 13, 14, 15}
 print("B=%d T=%d W=%d P=%d C=%d decode_ms=%.1f" % (B, T, W, P, C, d.last_stats["decode_kernel_ms"]))
 for k in range(16):
