@@ -1194,16 +1194,11 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
           continue;
         }
       }
-    } else if (full && (li0 == 0 || Cm1 >= 64)) {
-      const T ot0 = sel(cx.ot, buf)[i0];
-      if (li0 == 0 && uni((int)!(ot0 > bottom))) break;   // branch i0's turn: skipped, and all later
-      // (small C: a branch spans few chunks, and the chunk test below suffices)
-      if (!BIG && Cm1 >= 64 && uni((int)(!(pmax + ot0 > bottom) && cx.bloom[i0] == 0ull))) {
-        ++i0;   // (unreachable: C <= 64 here; kept so the small-C loop compiles as before)
-        li0 = 0;
-        continue;
-      }
     }
+    // small C: the turn check of a branch starting at this chunk's lane 0 uses
+    // that lane's total from the chunk's read batch below (a branch spans few
+    // chunks, and the chunk test below suffices for the rest)
+    const bool turn0 = !BIG && full && li0 == 0;
     const uint64_t tc0 = pc ? __builtin_amdgcn_s_memtime() : 0;
     // lane -> (branch, label index): x / Cm1 for x < 64 + Cm1, by float reciprocal
     const int x = li0 + lane;
@@ -1216,13 +1211,21 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     const int li = valid ? x - q * Cm1 : 0;
     for (li0 += 64; li0 >= Cm1; li0 -= Cm1) ++i0;
     const int l = li + (li >= blank ? 1 : 0);
+    // one batch of LDS reads, every lane (i is a valid branch, l a valid
+    // label), so the chunk waits on LDS once before its skip test
     const int bl = sel(cx.lab, buf)[i];
     const int bflg = sel(cx.flg, buf)[i];
     const T bt = sel(cx.ot, buf)[i];
-    bool live = valid && !(cx.bst[i] & S_DEACT);
+    const T bob = sel(cx.ob, buf)[i];
+    const int bsti = cx.bst[i];
+    const uint64_t blm = cx.bloom[i];
+    const int hd = cx.head[i];
+    const T bcb = sel(cx.cb, buf)[i], bcn = sel(cx.cn, buf)[i];
     const T xl = cx.row[l];
+    if (turn0 && !(bcast(bt, 0) > bottom)) break;   // branch i0's turn: skipped, and all later
+    bool live = valid && !(bsti & S_DEACT);
     const T p = xl - norm;
-    T base = (l == bl) ? sel(cx.ob, buf)[i] : bt;
+    T base = (l == bl) ? bob : bt;
     T cst = T(0);   // the child's scorer state (ExpandState, decoder.h:171)
     if constexpr (SC::kStateful) {
       cst = SC::expand(cx, sel(cx.est, buf)[i], bl, l);
@@ -1236,23 +1239,33 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     T bat = sl > 0 ? bottom : NI;
     const uint64_t startsM = __ballot(valid && li == 0 && lane != 0);   // branch turns starting mid-chunk
     if (pc) pc[10] += __builtin_amdgcn_s_memtime() - tc0;
-    if (full && !__ballot(live && (s > bottom || ((cx.bloom[i] >> (l & 63)) & 1ull)))) {
+    if (full && !__ballot(live && ((s > bottom) | (((blm >> (l & 63)) & 1ull) != 0)))) {
       if (startsM & ~__ballot(bt > bottom)) break;   // no event here: every start sees this bottom
       continue;
     }
+    // the branch child this offer re-offers, if any (GetChild finds it): walk
+    // branch i's children, each step one read pair (label, next sibling)
     int c = -1;
-    if (live) {
-      for (int k = cx.head[i]; k >= 0; k = cx.sib[k])
-        if (sel(cx.lab, buf)[k] == l) { c = k; break; }
+    for (int k = live ? hd : -1; __ballot(k >= 0);) {
+      int nk = -1;
+      if (k >= 0) {
+        const int lk = sel(cx.lab, buf)[k];
+        const int sk = cx.sib[k];
+        if (lk == l) c = k;
+        else nk = sk;
+      }
+      k = nk;
     }
     const bool isbc = c >= 0;
-    bool cev = isbc && (cx.bst[c] & S_EVICT);
-    // label-ending candidate for the child (decoder.h:172-185)
-    const bool recv_fresh = isbc ? (sel(cx.ot, buf)[c] == NI) : true;
+    const int cc = isbc ? c : i;
+    bool cev = isbc && (cx.bst[cc] & S_EVICT);
+    // label-ending candidate for the child (decoder.h:172-185), from branch i's
+    // candidates read in the batch above
+    const bool recv_fresh = isbc ? (sel(cx.ot, buf)[cc] == NI) : true;
     const T rs_blank = ((bflg & F_ROOT) && recv_fresh) ? T(0) : NI;
     Best<T> cd{T(0), kBpNone, false};
-    cand_from(cx, buf, i, 0, p, rs_blank, cd);
-    if (l != bl) cand_from(cx, buf, i, 1, p, NI, cd);
+    cd.push(((bflg & F_HB) ? bcb : rs_blank) + p, (bflg & F_HB) ? (((uint32_t)i << 1) | 0u) : kBpRestart);
+    if (l != bl) cd.push(((bflg & F_HN) ? bcn : NI) + p, (bflg & F_HN) ? (((uint32_t)i << 1) | 1u) : kBpRestart);
     const uint64_t isbm = __ballot(isbc);
 
     uint64_t tc1 = pc ? __builtin_amdgcn_s_memtime() : 0;
