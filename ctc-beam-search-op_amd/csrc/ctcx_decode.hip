@@ -899,6 +899,133 @@ __device__ __forceinline__ int heap_events_f32(float s, int c, int sl, unsigned 
   return st;
 }
 
+// The same event loop over one half of a 128-offer window (exact_step's
+// window path): the current half's offers are s/c/sl/myslot/bat and its lane
+// masks, the other half's appear only in the bookkeeping -- an evicted front
+// can be an entry the other half accepted (myo), and while the first half runs
+// (OTHER) a branch eviction makes the second half's re-offer of it wanted (rbo)
+// and its turns still to start see every new front (bato).  sl is
+// window-relative (0..127); hoff is the half's first window position.
+#define CTCX_HEV2_ASM(EVB_OTHER, BAT_OTHER)                                                                   \
+  asm volatile(                                                                                              \
+      "s_mov_b32 %[st], 0\n\t"                                                                               \
+      "v_cmp_lt_f32_e64 s[88:89], %[fv], %[s]\n\t"                                                           \
+      "s_and_b64 s[88:89], s[88:89], %[nc]\n\t"                                                              \
+      "s_or_b64 s[88:89], s[88:89], %[rb]\n\t"                                                               \
+      "s_andn2_b64 s[88:89], s[88:89], %[done]\n\t"                                                          \
+      "s_cbranch_scc0 .Lew_exit_%=\n\t"                                                                      \
+      "s_ff1_i32_b64 %[k], s[88:89]\n\t"                                                                     \
+      "s_bitcmp1_b64 %[lb], %[k]\n\t"                                                                        \
+      "s_cbranch_scc1 .Lew_rare_%=\n\t"                                                                      \
+      "ds_read_b128 v[232:235], %[al]\n\t"                                                                   \
+      "s_branch .Lew_tail_%=\n"                                                                              \
+      ".Lew_loop_%=:\n\t" CTCX_EVCNT                                                                         \
+      "s_waitcnt lgkmcnt(0)\n\t"                                                                             \
+      "v_cmp_ngt_f32_e64 s[92:93], v234, v232\n\t"                                                           \
+      "v_mov_b32_e32 v240, s84\n\t"                                                                          \
+      "v_mov_b32_e32 v241, s85\n\t"                                                                          \
+      "v_cndmask_b32_e64 v237, v232, v234, s[92:93]\n\t"                                                     \
+      "v_cndmask_b32_e64 v238, v233, v235, s[92:93]\n\t"                                                     \
+      "v_xor_b32_e32 v239, s92, %[req]\n\t"                                                                  \
+      "v_cmp_lt_f32_e64 s[96:97], s84, v237\n\t"                                                             \
+      "v_and_b32_e32 v239, v239, %[anc]\n\t"                                                                 \
+      "v_readfirstlane_b32 s86, v237\n\t"                                                                    \
+      "v_cmp_eq_u32_e64 s[94:95], 0, v239\n\t"                                                               \
+      "v_readfirstlane_b32 s87, v238\n\t"                                                                    \
+      "s_and_b64 s[98:99], s[92:93], %[k31]\n\t"                                                             \
+      "s_or_b64 s[98:99], s[98:99], %[khi]\n\t"                                                              \
+      "s_bitcmp1_b32 s96, 0\n\t"                                                                             \
+      "s_cselect_b32 %[fv], s84, s86\n\t"                                                                    \
+      "s_cselect_b32 %[fs], s85, s87\n\t"                                                                    \
+      "s_or_b64 s[98:99], s[98:99], s[96:97]\n\t"                                                            \
+      "s_add_u32 s85, %[k], %[hoff]\n\t"                                                                     \
+      "v_cmp_lt_i32_e64 vcc, s85, %[sl]\n\t"                                                                 \
+      "v_cmp_lt_f32_e64 s[88:89], %[fv], %[s]\n\t"                                                           \
+      "s_and_b64 s[90:91], s[94:95], s[98:99]\n\t"                                                           \
+      "s_ff1_i32_b64 s86, s[90:91]\n\t"                                                                      \
+      "v_mov_b32_e32 v242, %[fv]\n\t"                                                                        \
+      "s_lshl_b64 s[90:91], -2, s86\n\t"                                                                     \
+      "s_andn2_b64 s[94:95], s[94:95], s[90:91]\n\t"                                                         \
+      "s_andn2_b64 s[90:91], s[94:95], s[96:97]\n\t"                                                         \
+      "s_lshl_b64 s[94:95], 1, s86\n\t"                                                                      \
+      "v_cndmask_b32_e32 %[bat], %[bat], v242, vcc\n\t" BAT_OTHER                                           \
+      "v_cndmask_b32_e64 v236, %[al], %[ar], s[92:93]\n\t"                                                   \
+      "v_cndmask_b32_e64 v239, %[dum], %[aj], s[90:91]\n\t"                                                  \
+      "v_cndmask_b32_e64 v236, v236, %[aj], s[96:97]\n\t"                                                    \
+      "ds_write2_b32 v239, v237, v238 offset1:1\n\t"                                                         \
+      "v_cndmask_b32_e64 v236, %[dum], v236, s[94:95]\n\t"                                                   \
+      "s_and_b64 s[88:89], s[88:89], %[nc]\n\t"                                                              \
+      "s_or_b64 s[88:89], s[88:89], %[rb]\n\t"                                                               \
+      "ds_write2_b32 v236, v240, v241 offset1:1\n\t"                                                         \
+      "ds_read_b128 v[232:235], %[al]\n\t"                                                                   \
+      "s_andn2_b64 s[88:89], s[88:89], %[done]\n\t"                                                          \
+      "s_cbranch_scc0 .Lew_exit_%=\n\t"                                                                      \
+      "s_ff1_i32_b64 %[k], s[88:89]\n\t"                                                                     \
+      "s_bitcmp1_b64 %[lb], %[k]\n\t"                                                                        \
+      "s_cbranch_scc1 .Lew_rare_%=\n"                                                                        \
+      ".Lew_tail_%=:\n\t"                                                                                    \
+      "s_lshl_b64 s[90:91], -2, %[k]\n\t"                                                                    \
+      "s_not_b64 %[done], s[90:91]\n\t"                                                                      \
+      "v_readlane_b32 s84, %[s], %[k]\n\t"                                                                   \
+      "s_mov_b32 s85, %[fs]\n\t"                                                                             \
+      "s_cmp_lt_i32 %[fs], %[nb]\n\t"                                                                        \
+      "s_cbranch_scc1 .Lew_evb_%=\n"                                                                         \
+      ".Lew_slot_%=:\n\t"                                                                                    \
+      "v_cmp_eq_u32_e64 s[90:91], %[fs], %[my]\n\t"                                                          \
+      "v_cmp_eq_u32_e64 s[86:87], %[fs], %[myo]\n\t"                                                         \
+      "s_lshl_b64 vcc, 1, %[k]\n\t"                                                                          \
+      "v_mov_b32_e32 v243, s85\n\t"                                                                          \
+      "v_cndmask_b32_e64 %[my], %[my], -1, s[90:91]\n\t"                                                     \
+      "v_cndmask_b32_e64 %[myo], %[myo], -1, s[86:87]\n\t"                                                   \
+      "v_cndmask_b32_e32 %[my], %[my], v243, vcc\n\t"                                                        \
+      "s_branch .Lew_loop_%=\n"                                                                              \
+      ".Lew_evb_%=:\n\t"                                                                                     \
+      "s_mov_b32 s85, %[nfree]\n\t"                                                                          \
+      "s_add_u32 %[nfree], %[nfree], 1\n\t"                                                                  \
+      "s_lshl_b64 s[90:91], 1, %[nv]\n\t"                                                                    \
+      "v_mov_b32_e32 v243, %[fs]\n\t"                                                                        \
+      "s_add_u32 %[nv], %[nv], 1\n\t"                                                                        \
+      "v_cndmask_b32_e64 %[evr], %[evr], v243, s[90:91]\n\t"                                                 \
+      "v_cmp_eq_u32_e64 s[90:91], %[fs], %[c]\n\t"                                                           \
+      "s_and_b64 s[90:91], s[90:91], %[lb]\n\t"                                                              \
+      "s_or_b64 %[rb], %[rb], s[90:91]\n\t" EVB_OTHER                                                        \
+      "s_branch .Lew_slot_%=\n"                                                                              \
+      ".Lew_rare_%=:\n\t"                                                                                    \
+      "s_mov_b32 %[st], 1\n"                                                                                 \
+      ".Lew_exit_%=:\n\t"                                                                                    \
+      "s_waitcnt lgkmcnt(0)"                                                                                 \
+      : [my] "+v"(myslot), [myo] "+v"(myo), [evr] "+v"(evr), [bat] "+v"(bat), [bato] "+v"(bato),            \
+        [nc] "+s"(NC), [rb] "+s"(RB), [rbo] "+s"(RBo), [done] "+s"(done), [fv] "+s"(fv), [fs] "+s"(fs),     \
+        [nfree] "+s"(nfree), [nv] "+s"(nv), [k] "=&s"(k), [st] "=&s"(st), [cnt] "+s"(cnt)                    \
+      : [s] "v"(s), [c] "v"(c), [sl] "v"(sl), [co] "v"(co), [slo] "v"(slo), [anc] "v"(anc), [req] "v"(req),  \
+        [aj] "v"(aj), [al] "v"(al), [ar] "v"(ar), [dum] "v"(dum), [lb] "s"(LB), [lbo] "s"(LBo), [nb] "s"(nb), \
+        [hoff] "s"(hoff), [k31] "s"(k31), [khi] "s"(khi)                                                     \
+      : "memory", "vcc", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95",  \
+        "s96", "s97", "s98", "s99", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239", "v240",   \
+        "v241", "v242", "v243", "v244")
+
+template <bool OTHER>
+__device__ __forceinline__ int heap_events2_f32(float s, int c, int sl, int co, int slo, unsigned anc, unsigned req,
+                                                unsigned aj, unsigned al, unsigned ar, unsigned dum, int& myslot,
+                                                int& myo, int& evr, float& bat, float& bato, uint64_t& NC,
+                                                uint64_t& RB, uint64_t& RBo, uint64_t& done, uint64_t LB,
+                                                uint64_t LBo, float& fv, int& fs, int& nfree, int& nv, int nb,
+                                                int hoff, int& k, int& cnt) {
+  int st;
+  const uint64_t k31 = 0x80000000ull, khi = 0xffffffff00000000ull;
+  if constexpr (OTHER)
+    CTCX_HEV2_ASM("v_cmp_eq_u32_e64 s[90:91], %[fs], %[co]\n\t"
+                  "s_and_b64 s[90:91], s[90:91], %[lbo]\n\t"
+                  "s_or_b64 %[rbo], %[rbo], s[90:91]\n\t",
+                  "v_cmp_lt_i32_e64 s[86:87], s85, %[slo]\n\t"
+                  "v_mov_b32_e32 v244, %[fv]\n\t"
+                  "s_nop 1\n\t"
+                  "v_cndmask_b32_e64 %[bato], %[bato], v244, s[86:87]\n\t");
+  else
+    CTCX_HEV2_ASM("", "");
+  return st;
+}
+
 // sort_heap for float beams of up to 128 (exact_step's Extract), pops
 // pop_heap(len) for len = hi down to lo + 1 as one hand-scheduled asm loop:
 // the front goes to position len - 1 -- recorded as lane (len - 1 - base) of
@@ -1110,6 +1237,217 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
   int i0 = 0, li0 = 0;   // the chunk's first offer: branch i0, label index li0
   bool stop = false;
   while (i0 < nb && !stop) {
+    if constexpr (RN == 1 && !BIG && sizeof(T) == 4 && !SC::kStateful) {
+      if (st == kTopHeap && W >= 2) {
+        // ---- HEAP_SORTED, C <= 64, float: 128-offer windows (two halves of
+        // 64 lanes).  The same offer semantics as the 64-offer chunk below,
+        // with window positions 0..127 in place of lanes: one batch of reads,
+        // one skip test, one child walk and one flush per window, and the
+        // events of the first half, then the second, in one register state.
+        const uint64_t tc0 = pc ? __builtin_amdgcn_s_memtime() : 0;
+        const bool turnw = (li0 == 0);
+        int wi[2], wli[2], wl[2];
+        bool wv[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int x = li0 + lane + 64 * h;
+          int q = (int)((float)x * rcp);
+          q -= (q * Cm1 > x) ? 1 : 0;
+          q += ((q + 1) * Cm1 <= x) ? 1 : 0;
+          const int iv = i0 + q;
+          wv[h] = iv < nb;
+          wi[h] = wv[h] ? iv : i0;
+          wli[h] = wv[h] ? x - q * Cm1 : 0;
+          wl[h] = wli[h] + (wli[h] >= blank ? 1 : 0);
+        }
+        for (li0 += 128; li0 >= Cm1; li0 -= Cm1) ++i0;
+        int bl[2], bflg[2], bsti[2], hd[2];
+        T bt[2], bob[2], bcb[2], bcn[2], xl[2];
+        uint64_t blm[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int ii = wi[h];
+          bl[h] = sel(cx.lab, buf)[ii];
+          bflg[h] = sel(cx.flg, buf)[ii];
+          bt[h] = sel(cx.ot, buf)[ii];
+          bob[h] = sel(cx.ob, buf)[ii];
+          bsti[h] = cx.bst[ii];
+          blm[h] = cx.bloom[ii];
+          hd[h] = cx.head[ii];
+          bcb[h] = sel(cx.cb, buf)[ii];
+          bcn[h] = sel(cx.cn, buf)[ii];
+          xl[h] = cx.row[wl[h]];
+        }
+        if (turnw && !(bcast(bt[0], 0) > bottom)) break;   // branch i0's turn: skipped, and all later
+        bool wlive[2];
+        T sw[2], pw[2], batw[2];
+        int slw[2];
+        uint64_t stM[2], wantM[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          wlive[h] = wv[h] && !(bsti[h] & S_DEACT);
+          pw[h] = xl[h] - norm;
+          sw[h] = pw[h] + ((wl[h] == bl[h]) ? bob[h] : bt[h]);
+          slw[h] = lane + 64 * h - wli[h];   // window position where the lane's branch turn starts
+          batw[h] = slw[h] > 0 ? bottom : NI;
+          stM[h] = __ballot(wv[h] && wli[h] == 0 && lane + 64 * h != 0);
+          wantM[h] = __ballot(wlive[h] && ((sw[h] > bottom) | (((blm[h] >> (wl[h] & 63)) & 1ull) != 0)));
+        }
+        if (pc) pc[10] += __builtin_amdgcn_s_memtime() - tc0;
+        if (!(wantM[0] | wantM[1])) {
+          if ((stM[0] & ~__ballot(bt[0] > bottom)) | (stM[1] & ~__ballot(bt[1] > bottom))) break;
+          continue;
+        }
+        int cw[2] = {-1, -1};
+        {
+          int k0 = wlive[0] ? hd[0] : -1, k1 = wlive[1] ? hd[1] : -1;
+          while (__ballot(k0 >= 0 || k1 >= 0)) {
+            int n0 = -1, n1 = -1;
+            if (k0 >= 0) {
+              const int lk = sel(cx.lab, buf)[k0];
+              const int sk = cx.sib[k0];
+              if (lk == wl[0]) cw[0] = k0;
+              else n0 = sk;
+            }
+            if (k1 >= 0) {
+              const int lk = sel(cx.lab, buf)[k1];
+              const int sk = cx.sib[k1];
+              if (lk == wl[1]) cw[1] = k1;
+              else n1 = sk;
+            }
+            k0 = n0;
+            k1 = n1;
+          }
+        }
+        Best<T> cdw[2];
+        uint64_t NCw[2], LBw[2], RBw[2], donew[2] = {0ull, 0ull};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const bool isbc = cw[h] >= 0;
+          const int cc = isbc ? cw[h] : wi[h];
+          const bool cev = isbc && (cx.bst[cc] & S_EVICT);
+          const bool recv_fresh = isbc ? (sel(cx.ot, buf)[cc] == NI) : true;
+          const T rs_blank = ((bflg[h] & F_ROOT) && recv_fresh) ? T(0) : NI;
+          cdw[h] = Best<T>{T(0), kBpNone, false};
+          cdw[h].push(((bflg[h] & F_HB) ? bcb[h] : rs_blank) + pw[h],
+                      (bflg[h] & F_HB) ? (((uint32_t)wi[h] << 1) | 0u) : kBpRestart);
+          if (wl[h] != bl[h])
+            cdw[h].push(((bflg[h] & F_HN) ? bcn[h] : NI) + pw[h],
+                        (bflg[h] & F_HN) ? (((uint32_t)wi[h] << 1) | 1u) : kBpRestart);
+          const uint64_t liveM = __ballot(wlive[h]), isbm = __ballot(isbc);
+          NCw[h] = liveM & ~isbm;
+          LBw[h] = liveM & isbm;
+          RBw[h] = LBw[h] & __ballot(cev);
+        }
+        const uint64_t tc1 = pc ? __builtin_amdgcn_s_memtime() : 0;
+        if (pc) { pc[8] += tc1 - tc0; pc[11] += 1; }
+        int mys[2] = {-1, -1};
+        int evr = 0, nv = 0;
+        T fv = front.v;
+        int fs = front.s;
+        int nfree = nextfree;
+        const HeapM geo = heap_m(cx.hdum);
+        const unsigned heb = (unsigned)(uintptr_t)he;
+        const unsigned aj = heb + 8u * (unsigned)(lane + 1), al = heb + 8u * (unsigned)(2 * lane + 2);
+        const unsigned ar = al + 8u, dum = heb + 8u * (unsigned)(cx.hdum + lane);
+        // the events of half H (other half O); rare ones (re-offered branch
+        // children) are decided here, as in the chunk loop below
+#define CTCX_WIN_HALF(H, O)                                                                                       \
+        for (;;) {                                                                                                \
+          int k, cnt = 0;                                                                                         \
+          fv = uni(fv); fs = uni(fs); nfree = uni(nfree); nv = uni(nv);                                           \
+          const uint64_t ta = pc ? __builtin_amdgcn_s_memtime() : 0;                                              \
+          const int est = heap_events2_f32<H == 0>(sw[H], cw[H], slw[H], cw[O], slw[O], geo.anc, geo.req, aj,   \
+                                                   al, ar, dum, mys[H], mys[O], evr, batw[H], batw[O], NCw[H],   \
+                                                   RBw[H], RBw[O], donew[H], LBw[H], LBw[O], fv, fs, nfree, nv,  \
+                                                   uni(nb), 64 * H, k, cnt);                                     \
+          if (pc) { pc[13] += __builtin_amdgcn_s_memtime() - ta; pc[6] += uni(cnt); pc[12] += 1; }             \
+          if (est == 0) break;                                                                                    \
+          k = uni(k);                                                                                             \
+          const uint64_t gtM = __ballot(sw[H] > fv);                                                             \
+          const uint64_t m = ((gtM & NCw[H]) | RBw[H]) & ~donew[H];                                              \
+          if ((__ballot(!(bt[H] > batw[H])) >> k) & 1ull) {                                                      \
+            const int ksl = bcast(slw[H], k);                                                                     \
+            const uint64_t km0 = lowmask(ksl), km1 = ksl > 64 ? lowmask(ksl - 64) : 0ull;                        \
+            NCw[0] &= km0; LBw[0] &= km0; RBw[0] &= km0;                                                          \
+            NCw[1] &= km1; LBw[1] &= km1; RBw[1] &= km1;                                                          \
+            stop = true;                                                                                          \
+            continue;                                                                                             \
+          }                                                                                                       \
+          donew[H] = m ^ (m - 1ull);                                                                              \
+          const int kc = bcast(cw[H], k);                                                                         \
+          if (!((gtM >> k) & 1ull)) {                                                                             \
+            evr = writelane(evr, kc | kDeactRec, nv);                                                             \
+            nv += 1;                                                                                              \
+            const uint64_t dm0 = ~__ballot(wi[0] == kc), dm1 = ~__ballot(wi[1] == kc);                            \
+            NCw[0] &= dm0; LBw[0] &= dm0; RBw[0] &= dm0;                                                          \
+            NCw[1] &= dm1; LBw[1] &= dm1; RBw[1] &= dm1;                                                          \
+            continue;                                                                                             \
+          }                                                                                                       \
+          if (fs < nb) {                                                                                          \
+            evr = writelane(evr, fs, nv);                                                                         \
+            nv += 1;                                                                                              \
+            RBw[0] |= LBw[0] & __ballot(cw[0] == fs);                                                             \
+            RBw[1] |= LBw[1] & __ballot(cw[1] == fs);                                                             \
+          }                                                                                                       \
+          const T k_s = bcast(sw[H], k);                                                                          \
+          mys[0] = (mys[0] == fs) ? -1 : mys[0];                                                                  \
+          mys[1] = (mys[1] == fs) ? -1 : mys[1];                                                                  \
+          mys[H] = __builtin_amdgcn_inverse_ballot_w64(1ull << k) ? kc : mys[H];                                 \
+          HE<T> pL, pR;                                                                                           \
+          pairs_m(he, geo, pL, pR);                                                                               \
+          T c0;                                                                                                   \
+          int s0;                                                                                                 \
+          bool keep;                                                                                              \
+          push_m<T>(he, geo, k_s, kc, pL, pR, c0, s0, keep);                                                      \
+          fv = keep ? k_s : c0;                                                                                   \
+          fs = keep ? kc : s0;                                                                                    \
+          const int kp = k + 64 * H;                                                                              \
+          batw[0] = (slw[0] > kp) ? fv : batw[0];                                                                 \
+          batw[1] = (slw[1] > kp) ? fv : batw[1];                                                                 \
+        }
+        CTCX_WIN_HALF(0, 1)
+        donew[0] = ~0ull;   // the first half's offers are all behind
+        CTCX_WIN_HALF(1, 0)
+#undef CTCX_WIN_HALF
+        front.v = fv;
+        front.s = fs;
+        bottom = fv;
+        nextfree = nfree;
+        // the turn continuing into the next window: skipped -> so is every later one
+        if ((__ballot(wv[1] && !(bt[1] > batw[1])) >> 63) & 1ull) stop = true;
+        const uint64_t q5 = pc ? __builtin_amdgcn_s_memtime() : 0;
+        if (lane < nv) {
+          const int rs = evr & ~kDeactRec;
+          if (evr & kDeactRec) {
+            __hip_atomic_fetch_or(&cx.bst[rs], S_DEACT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          } else {
+            cx.et[rs] = NI; cx.eb[rs] = NI; cx.el[rs] = NI; cx.eflg[rs] = 0;
+            __hip_atomic_fetch_or(&cx.bst[rs], S_EVICT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const int par = sel(cx.par, buf)[rs];
+            if (par >= 0)
+              __hip_atomic_fetch_or(&cx.bloom[par], 1ull << (sel(cx.lab, buf)[rs] & 63), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int ms = mys[h];
+          if (ms >= 0) {
+            const bool isbc = cw[h] >= 0;
+            cx.et[ms] = sw[h]; cx.eb[ms] = NI; cx.el[ms] = sw[h];
+            cx.ecn[ms] = cdw[h].p; cx.ebpn[ms] = cdw[h].bp;
+            cx.eflg[ms] = F_HN;
+            cx.ekind[ms] = isbc ? ((uint32_t)cw[h] << 1) : (((uint32_t)wi[h] << 1) | 1u);
+            cx.elab[ms] = wl[h];
+            if (isbc) __hip_atomic_fetch_and(&cx.bst[cw[h]], ~S_EVICT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+        }
+        if (pc) pc[15] += __builtin_amdgcn_s_memtime() - q5;
+        if (pc) pc[9] += __builtin_amdgcn_s_memtime() - tc1;
+        continue;
+      }
+    }
     if (BIG && full) {
       // large C, lane-parallel: lane j tests branch i0 + j (its turn skipped:
       // stop; its rest skippable whole: pmax + ot <= bottom, bloom clear), and
