@@ -82,6 +82,9 @@ __device__ __forceinline__ float uni(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
 }
 __device__ __forceinline__ double uni(double v) { return bcast(v, 0); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return ((uint64_t)(uint32_t)uni((int)(v >> 32)) << 32) | (uint32_t)uni((int)(uint32_t)v);
+}
 
 template <typename T>
 __device__ __forceinline__ T wave_min(T v) {
@@ -1013,6 +1016,9 @@ __device__ __forceinline__ int heap_events2_f32(float s, int c, int sl, int co, 
                                                 int hoff, int& k, int& cnt) {
   int st;
   const uint64_t k31 = 0x80000000ull, khi = 0xffffffff00000000ull;
+  // every scalar operand provably uniform (the asm's "s" constraints)
+  NC = uni64(NC); RB = uni64(RB); RBo = uni64(RBo); done = uni64(done); LB = uni64(LB); LBo = uni64(LBo);
+  fv = uni(fv); fs = uni(fs); nfree = uni(nfree); nv = uni(nv); nb = uni(nb); hoff = uni(hoff); cnt = uni(cnt);
   if constexpr (OTHER)
     CTCX_HEV2_ASM("v_cmp_eq_u32_e64 s[90:91], %[fs], %[co]\n\t"
                   "s_and_b64 s[90:91], s[90:91], %[lbo]\n\t"
