@@ -1,4 +1,5 @@
+#!/bin/bash
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-CTCEXT_LIB_PATH=$PWD/tools/libctcext_phases.so timeout -k 10 300 python tools/diag_phases.py 256 1500 128 3 > gpurun_out/phases7.txt 2>&1
-timeout -k 10 400 bash tools/abn.sh 1 abv/new9.so abv/new10.so > gpurun_out/ab10.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r2d_pytest.log 2>&1 || exit 21
+QUICK=${QUICK:-0} TAG=r2d bash tools/profile_round.sh
