@@ -197,6 +197,19 @@ template <typename T>
 __host__ __device__ __forceinline__ CTCX_LDS T* row_bmax(const Ctx<T>& cx) {
   return (CTCX_LDS T*)((CTCX_LDS char*)cx.row + (((size_t)cx.C * sizeof(T) + 15) & ~(size_t)15));
 }
+// Large C, after the block maxima: the compacted chunk's offers (64 x (branch
+// << 16 | label index)), then the label-index bitmap of the children of one
+// branch (bit x of word x >> 6) and its per-window summary (bit a of word
+// a >> 6: window a holds a child).  Layout as in decode_lds_bytes.
+template <typename T>
+__host__ __device__ __forceinline__ CTCX_LDS uint32_t* row_cq(const Ctx<T>& cx) {
+  const size_t nblk = (size_t)(cx.C + 63) / 64;
+  return (CTCX_LDS uint32_t*)((CTCX_LDS char*)row_bmax(cx) + ((nblk * sizeof(T) + 15) & ~(size_t)15));
+}
+template <typename T>
+__host__ __device__ __forceinline__ CTCX_LDS uint64_t* row_cbm(const Ctx<T>& cx) {
+  return (CTCX_LDS uint64_t*)(row_cq(cx) + 64);
+}
 
 // Frame-parity buffer select without indexing the pointer pair, so Ctx stays
 // in registers (a runtime index into a member array would force it to scratch).
@@ -1142,6 +1155,40 @@ __device__ HE<T> wave_first_min_to_front(CTCX_LDS HE<T>* he, int n) {
 // then peeks lazily; rare: only while the beam is still filling).
 // On success cx.sorted[0..*n_out) holds the Extract() order and, for the last
 // frame, cx.tops[0..min(P, leaves)) the TopPaths() selection as positions.
+// Large C: move the child bitmap and its window summary from branch ob's
+// children to branch nb_'s (-1: none).  The children of a branch are the
+// branches whose parent it is (the child list head/sib is built from par);
+// every erase is issued before any record (one wave: LDS keeps that order).
+template <typename T>
+__device__ __forceinline__ void cq_children(const Ctx<T>& cx, int buf, int nb, int ob, int nb_) {
+  CTCX_LDS uint64_t* cbm = row_cbm(cx);
+  CTCX_LDS uint64_t* cwin = cbm + (cx.C - 1 + 63) / 64;
+  if (ob >= 0) {
+    for (int k = threadIdx.x; k < nb; k += 64) {
+      const int pk = sel(cx.par, buf)[k];
+      const int lk = sel(cx.lab, buf)[k];
+      if (pk == ob) {
+        const int x = lk - (lk > cx.blank ? 1 : 0);
+        cbm[x >> 6] = 0ull;
+        cwin[x >> 12] = 0ull;
+      }
+    }
+  }
+  if (nb_ >= 0) {
+    for (int k = threadIdx.x; k < nb; k += 64) {
+      const int pk = sel(cx.par, buf)[k];
+      const int lk = sel(cx.lab, buf)[k];
+      if (pk == nb_) {
+        const int x = lk - (lk > cx.blank ? 1 : 0);
+        __hip_atomic_fetch_or(&cbm[x >> 6], 1ull << (x & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_or(&cwin[x >> 12], 1ull << ((x >> 6) & 63), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+  }
+}
+constexpr int kGatherWin = 8;   // kept 64-label windows per batch of row reads in the gather
+
 template <typename T, int RN, bool BIG, class SC>
 __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, bool last, int P, int* n_out,
                           int* n_leaves, uint64_t* pc) {
@@ -1242,6 +1289,10 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
   const float rcp = 1.0f / (float)Cm1;
   int i0 = 0, li0 = 0;   // the chunk's first offer: branch i0, label index li0
   bool stop = false;
+  // large C (compacted chunks): the gathered offers, the span's first offer,
+  // a closed turn found by the gather, the branch whose children the bitmap holds
+  int cqn = 0, cq_i0 = 0, cq_l0 = 0, cbr = -1;
+  bool gstop = false;
   while (i0 < nb && !stop) {
     if constexpr (RN == 1 && !BIG && sizeof(T) == 4 && !SC::kStateful) {
       if (st == kTopHeap && W >= 2) {
@@ -1454,50 +1505,81 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
         continue;
       }
     }
+    // large C, the beam full: a compacted chunk.  The offers of the span from
+    // (i0, li0) on that can have an effect are gathered, in offer order, into
+    // cx.cq (up to 64): a new child whose score can beat the current bottom
+    // ((x_l - norm) + ot > bottom bounds the score; bottom only rises, so an
+    // offer failing it now fails at its turn too) and every re-offer of a branch
+    // child (evicted now, or by an event of this chunk before it).  The rest of
+    // the span is rejected by the reference without effect.  Branch turns are
+    // checked here at the current bottom (closed now: closed at its turn, the
+    // grow ends after this chunk) and again in the chunk at the bottom its turn
+    // sees (sl, bat below).
     if (BIG && full) {
-      // large C, lane-parallel: lane j tests branch i0 + j (its turn skipped:
-      // stop; its rest skippable whole: pmax + ot <= bottom, bloom clear), and
-      // the first branch that is neither skipped is where the scan resumes
-      // (the same per-branch tests, in the same order, 64 at a time)
-      int res = 0;   // 0: at a branch to scan, 1: a turn is skipped (stop), 2: past the last branch
-      T ot0 = NI;    // the found branch's total and bloom state, read out of its lane
-      bool bz0 = false;
-      for (;;) {
-        const int ib = i0 + lane;
-        bool brk = false, skp = true, bz = false;
-        T otb = NI;
-        if (ib < nb) {
-          otb = sel(cx.ot, buf)[ib];
-          bz = cx.bloom[ib] == 0ull;
-          brk = (lane > 0 || li0 == 0) && !(otb > bottom);
-          skp = !(pmax + otb > bottom) && bz;
+      CTCX_LDS uint32_t* cq = row_cq(cx);
+      CTCX_LDS uint64_t* cbm = row_cbm(cx);
+      CTCX_LDS uint64_t* cwin = cbm + (Cm1 + 63) / 64;
+      cq_i0 = i0;
+      cq_l0 = li0;
+      cqn = 0;
+      // the branch scan (lane j: branch sb + j) and a branch's window scan
+      // (lane w: window wa0 + w) hold for the whole gather: no event moves the
+      // bottom before the chunk runs
+      int sb = -1, wa0 = -1;
+      uint64_t hitM = 0, brkM = 0, chM = 0, wkM = 0;
+      T otb = NI, ot0 = NI;
+      bool enter = true;   // at the gather's start or a branch's first offer
+      while (cqn < 64) {
+        if (enter) {
+          // the next branch with a turn closed (stop), or with something to
+          // gather (pmax + ot > bottom, or children)
+          int res = 0;   // 0: at a branch to gather from, 1: a turn is closed, 2: past the last branch
+          for (;;) {
+            if (sb < 0 || i0 >= sb + 64) {
+              sb = i0;
+              const int ib = i0 + lane;
+              bool brk = false, skp = true, ch = false;
+              otb = NI;
+              if (ib < nb) {
+                otb = sel(cx.ot, buf)[ib];
+                ch = cx.head[ib] >= 0;
+                brk = (lane > 0 || li0 == 0) && !(otb > bottom);
+                skp = !(pmax + otb > bottom) && !ch;
+              }
+              hitM = __ballot(brk || !skp);
+              brkM = __ballot(brk);
+              chM = __ballot(ch);
+            }
+            const uint64_t m = hitM & ~lowmask(i0 - sb);
+            if (m == 0) {
+              i0 = sb + 64;
+              li0 = 0;
+              if (i0 >= nb) { res = 2; break; }
+              continue;
+            }
+            const int k = (int)__builtin_ctzll(m);
+            if (sb + k > i0) li0 = 0;
+            i0 = sb + k;
+            if ((brkM >> k) & 1ull) res = 1;
+            ot0 = bcast(otb, k);
+            const int nbr = ((chM >> k) & 1ull) ? i0 : -1;
+            if (nbr != cbr) {
+              cq_children(cx, buf, nb, cbr, nbr);
+              cbr = nbr;
+            }
+            break;
+          }
+          if (res == 1) gstop = true;
+          if (res != 0) break;
+          enter = false;
+          wa0 = -1;
         }
-        const uint64_t hitM = __ballot(brk || !skp);
-        if (hitM == 0) {
-          i0 += 64;
-          li0 = 0;
-          if (i0 >= nb) { res = 2; break; }
-          continue;
-        }
-        const int k = (int)__builtin_ctzll(hitM);
-        if (k > 0) li0 = 0;
-        i0 += k;
-        if ((__ballot(brk) >> k) & 1ull) res = 1;
-        bz0 = (__ballot(bz) >> k) & 1ull;
-        ot0 = bcast(otb, k);
-        break;
-      }
-      if (res == 1) break;
-      if (res == 2) continue;
-      if (bz0) {
-        // the branch's 64-offer windows, 64 windows per step (lane j: window
-        // li0 + 64 j): a window whose labels' block maxima bound every score
-        // (xb - norm) + ot0 <= bottom holds no accepted offer and no re-offer
-        // (bloom clear), so it is passed over (the chunk test below, at two
-        // LDS reads)
-        bool rest = false;
-        for (;;) {
-          const int lw = li0 + 64 * lane;
+        // branch i0's aligned 64-label windows from li0 on (lane w: window
+        // wa0 + w): one whose labels' block maxima bound every score
+        // (xb - norm) + ot0 <= bottom and that holds no child is passed over
+        if (wa0 < 0 || (li0 >> 6) >= wa0 + 64) {
+          wa0 = li0 >> 6;
+          const int lw = (wa0 + lane) * 64;
           bool keep = false;
           if (lw < Cm1) {
             const int le = (lw + 64 < Cm1 ? lw + 64 : Cm1) - 1;
@@ -1505,38 +1587,74 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
             const int lb = le + (le >= blank ? 1 : 0);
             const T ba = bmax[la >> 6], bb = bmax[lb >> 6];
             const T xb = ba > bb ? ba : bb;
-            keep = ((xb - norm) + ot0) > bottom;
+            const int a = wa0 + lane;
+            keep = (((xb - norm) + ot0) > bottom) || (((cwin[a >> 6] >> (a & 63)) & 1ull) != 0);
           }
-          const uint64_t keepM = __ballot(keep);
-          if (keepM) {
-            li0 += 64 * (int)__builtin_ctzll(keepM);
-            // within the kept window, the exact per-label bound
-            // (x_l - norm) + ot0 > bottom (>= the offer's score: ob <= ot):
-            // the chunk starts at the first label passing it, and a window
-            // where none passes is passed over as well
-            const int lx = li0 + lane;
-            bool hot = false;
-            if (lx < Cm1) {
-              const int l = lx + (lx >= blank ? 1 : 0);
-              hot = ((cx.row[l] - norm) + ot0) > bottom;
-            }
-            const uint64_t hotM = __ballot(hot);
-            if (hotM) {
-              li0 += (int)__builtin_ctzll(hotM);
-              break;
-            }
-            if (li0 + 64 >= Cm1) { rest = true; break; }
-            li0 += 64;
-            continue;
-          }
-          if (li0 + 64 * 64 >= Cm1) { rest = true; break; }
-          li0 += 64 * 64;
+          wkM = __ballot(keep);
         }
-        if (rest) {
+        uint64_t m = wkM & ~lowmask((li0 >> 6) - wa0);
+        int nli0;
+        if (m == 0) {
+          nli0 = (wa0 + 64) * 64;
+        } else {
+          // up to kGatherWin kept windows per batch of row reads: the exact
+          // per-label bound, and the children
+          int aw[kGatherWin];
+          T xv[kGatherWin];
+          uint64_t cw[kGatherWin];
+#pragma unroll
+          for (int j = 0; j < kGatherWin; ++j) {
+            aw[j] = -1;
+            if (m) {
+              aw[j] = wa0 + (int)__builtin_ctzll(m);
+              m &= m - 1ull;
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < kGatherWin; ++j) {
+            xv[j] = NI;
+            cw[j] = 0ull;
+            if (aw[j] >= 0) {
+              const int x = aw[j] * 64 + lane;
+              const int xc = x < Cm1 ? x : Cm1 - 1;
+              xv[j] = cx.row[xc + (xc >= blank ? 1 : 0)];
+              cw[j] = cbm[aw[j]];
+            }
+          }
+          nli0 = -1;
+          int endw = 0;
+#pragma unroll
+          for (int j = 0; j < kGatherWin; ++j) {
+            if (aw[j] >= 0 && nli0 < 0 && cqn < 64) {
+              const int wb = aw[j] * 64;
+              const int x = wb + lane;
+              const bool hot = x >= li0 && x < Cm1 &&
+                               ((((xv[j] - norm) + ot0) > bottom) || (((cw[j] >> lane) & 1ull) != 0));
+              uint64_t hotM = __ballot(hot);
+              const int rank =
+                  (int)__builtin_amdgcn_mbcnt_hi((unsigned)(hotM >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)hotM, 0u));
+              if (__builtin_popcountll(hotM) > 64 - cqn) {   // the chunk fills here
+                hotM = __ballot(hot && rank < 64 - cqn);
+                nli0 = wb + 64 - __builtin_clzll(hotM);
+              }
+              if ((hotM >> lane) & 1ull) cq[cqn + rank] = ((uint32_t)i0 << 16) | (uint32_t)x;
+              cqn += __builtin_popcountll(hotM);
+              endw = wb + 64;
+            }
+          }
+          if (nli0 < 0) nli0 = endw;
+        }
+        li0 = nli0;
+        if (li0 >= Cm1) {
           ++i0;
           li0 = 0;
-          continue;
+          enter = true;
+          if (i0 >= nb) break;
         }
+      }
+      if (cqn == 0) {
+        if (gstop) stop = true;
+        break;
       }
     }
     // small C: the turn check of a branch starting at this chunk's lane 0 uses
@@ -1544,16 +1662,34 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     // chunks, and the chunk test below suffices for the rest)
     const bool turn0 = !BIG && full && li0 == 0;
     const uint64_t tc0 = pc ? __builtin_amdgcn_s_memtime() : 0;
-    // lane -> (branch, label index): x / Cm1 for x < 64 + Cm1, by float reciprocal
-    const int x = li0 + lane;
-    int q = (int)((float)x * rcp);
-    q -= (q * Cm1 > x) ? 1 : 0;
-    q += ((q + 1) * Cm1 <= x) ? 1 : 0;
-    const int iv = i0 + q;
-    const bool valid = iv < nb;
-    const int i = valid ? iv : i0;
-    const int li = valid ? x - q * Cm1 : 0;
-    for (li0 += 64; li0 >= Cm1; li0 -= Cm1) ++i0;
+    bool valid;
+    int i, li, sl;   // sl: the lane where this lane's branch turn starts in the chunk (see bat below)
+    if (BIG && full) {
+      // the compacted chunk: lane j < cqn holds the j-th gathered offer; a
+      // branch turn starts at the first lane of its branch unless the branch
+      // began before the span
+      CTCX_LDS uint32_t* cq = row_cq(cx);
+      valid = lane < cqn;
+      const uint32_t e = cq[valid ? lane : 0];
+      const uint32_t ep = cq[lane > 0 ? lane - 1 : 0];
+      i = (int)(e >> 16);
+      li = (int)(e & 0xFFFFu);
+      const int ip = lane > 0 ? (int)(ep >> 16) : -1;
+      const uint64_t fm = __ballot(valid && i != ip) & lowmask(lane + 1);
+      sl = (i > cq_i0 || cq_l0 == 0) ? 63 - __builtin_clzll(fm) : -1;
+    } else {
+      // lane -> (branch, label index): x / Cm1 for x < 64 + Cm1, by float reciprocal
+      const int x = li0 + lane;
+      int q = (int)((float)x * rcp);
+      q -= (q * Cm1 > x) ? 1 : 0;
+      q += ((q + 1) * Cm1 <= x) ? 1 : 0;
+      const int iv = i0 + q;
+      valid = iv < nb;
+      i = valid ? iv : i0;
+      li = valid ? x - q * Cm1 : 0;
+      for (li0 += 64; li0 >= Cm1; li0 -= Cm1) ++i0;
+      sl = lane - li;
+    }
     const int l = li + (li >= blank ? 1 : 0);
     // one batch of LDS reads, every lane (i is a valid branch, l a valid
     // label), so the chunk waits on LDS once before its skip test
@@ -1576,15 +1712,15 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       base = SC::score(cst, base);
     }
     const T s = p + base;
-    // the lane where this lane's branch turn starts in the chunk (< 0: in an
-    // earlier chunk, found open there), and the bottom at that moment (bat:
+    // sl: the lane where this lane's branch turn starts in the chunk (< 0: in
+    // an earlier chunk, found open there), and the bottom at that moment (bat:
     // refreshed after every event for turns that start later in the chunk)
-    const int sl = lane - li;
     T bat = sl > 0 ? bottom : NI;
-    const uint64_t startsM = __ballot(valid && li == 0 && lane != 0);   // branch turns starting mid-chunk
+    const uint64_t startsM = __ballot(valid && sl == lane && lane != 0);   // branch turns starting mid-chunk
     if (pc) pc[10] += __builtin_amdgcn_s_memtime() - tc0;
     if (full && !__ballot(live && ((s > bottom) | (((blm >> (l & 63)) & 1ull) != 0)))) {
       if (startsM & ~__ballot(bt > bottom)) break;   // no event here: every start sees this bottom
+      if (gstop) break;
       continue;
     }
     // the branch child this offer re-offers, if any (GetChild finds it): walk
@@ -1904,7 +2040,8 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       }
     }
     // the turn continuing into the next chunk: skipped -> so is every later one
-    if (full && (__ballot(valid && !(bt > bat)) >> 63) & 1ull) stop = true;
+    if (full && (__ballot(valid && !(bt > bat)) >> ((BIG && full) ? cqn - 1 : 63)) & 1ull) stop = true;
+    if (gstop) stop = true;
     // flush: resets and flags first, then the surviving accepted entries
     const uint64_t q5 = pc ? __builtin_amdgcn_s_memtime() : 0;
     if (lane < nev) {
@@ -1933,6 +2070,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     if (pc) pc[9] += __builtin_amdgcn_s_memtime() - tc1;
   }
 
+  if (BIG && cbr >= 0) cq_children(cx, buf, nb, cbr, -1);
   uint64_t ts2 = pc ? __builtin_amdgcn_s_memtime() : 0;
   if (pc) pc[2] += ts2 - ts1;
   const int size = n < W ? n : W;
@@ -2207,6 +2345,11 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     cx.head[0] = -1;
     cx.alias[0] = 0;
     if constexpr (SC::kStateful) cx.est[0][0] = T(0);   // InitializeState (decoder.h:226)
+  }
+  if constexpr (BIG) {   // the child bitmap and window summary start (and stay, between branches) clear
+    const int nw = (C - 1 + 63) / 64;
+    CTCX_LDS uint64_t* z = row_cbm(cx);
+    for (int k = lane; k < nw + (nw + 63) / 64; k += 64) z[k] = 0ull;
   }
   int nb = 1;
   int literal_steps = 0;
