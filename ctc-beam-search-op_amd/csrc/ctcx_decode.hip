@@ -210,6 +210,12 @@ template <typename T>
 __host__ __device__ __forceinline__ CTCX_LDS uint64_t* row_cbm(const Ctx<T>& cx) {
   return (CTCX_LDS uint64_t*)(row_cq(cx) + 64);
 }
+// ... then the row's top set (float rows): values, label indices, 64 each
+template <typename T>
+__host__ __device__ __forceinline__ CTCX_LDS float* row_topx(const Ctx<T>& cx) {
+  const int nw = (cx.C - 1 + 63) / 64;
+  return (CTCX_LDS float*)(row_cbm(cx) + nw + (nw + 63) / 64);
+}
 
 // Frame-parity buffer select without indexing the pointer pair, so Ctx stays
 // in registers (a runtime index into a member array would force it to scratch).
@@ -1189,6 +1195,85 @@ __device__ __forceinline__ void cq_children(const Ctx<T>& cx, int buf, int nb, i
 }
 constexpr int kGatherWin = 8;   // kept 64-label windows per batch of row reads in the gather
 
+// Large C, float rows: the row's top set S = the non-blank labels whose value
+// is >= tau, for the smallest tau that leaves at most 64 of them (bisection
+// on the order-preserving integer key of the float), written in label-index
+// order to row_topx (values) and the int array after it (label indices).
+// Returns |S|; xout = the largest value outside S (-inf: none).  An offer
+// bound (x - norm) + ot is monotone in x, so when it fails for xout it fails
+// for every label outside S, and S alone holds the branch's candidates.
+template <typename T>
+__device__ __forceinline__ int row_top_set(const Ctx<T>& cx, T& xout) {
+  if constexpr (sizeof(T) != 4) {
+    xout = pinf<T>();
+    return 0;
+  } else {
+    const int lane = threadIdx.x;
+    const int Cm1 = cx.C - 1, blank = cx.blank;
+    auto key = [](float v) {
+      const unsigned b = __float_as_uint(v);
+      return b ^ ((b >> 31) ? 0xFFFFFFFFu : 0x80000000u);
+    };
+    auto kat = [&](int x) { return key(cx.row[x + (x >= blank ? 1 : 0)]); };
+    constexpr int KR = 16;   // rows of up to 64 * KR labels keep their keys in registers
+    unsigned kr[KR];
+    const bool inreg = Cm1 <= 64 * KR;
+#pragma unroll
+    for (int j = 0; j < KR; ++j) {
+      const int x = 64 * j + lane;
+      kr[j] = (inreg && x < Cm1) ? kat(x) : 0u;
+    }
+    auto cnt_ge = [&](unsigned tau) {
+      int c = 0;
+      if (inreg) {
+#pragma unroll
+        for (int j = 0; j < KR; ++j) {
+          const int x = 64 * j + lane;
+          c += __builtin_popcountll(__ballot(x < Cm1 && kr[j] >= tau));
+        }
+      } else {
+        for (int x0 = 0; x0 < Cm1; x0 += 64) {
+          const int x = x0 + lane;
+          c += __builtin_popcountll(__ballot(x < Cm1 && kat(x) >= tau));
+        }
+      }
+      return c;
+    };
+    // smallest tau with |{key >= tau}| <= 64: cnt(lo) > 64 >= cnt(hi)
+    uint64_t lo = 0, hi = 1ull << 32;
+    while (hi - lo > 1) {
+      const uint64_t mid = (lo + hi) >> 1;
+      const int c = cnt_ge((unsigned)mid);
+      if (c <= 64) hi = mid;
+      else lo = mid;
+      if (c == 64) break;
+    }
+    const unsigned tau = (unsigned)hi;
+    CTCX_LDS float* sx = row_topx(cx);
+    CTCX_LDS int* sli = (CTCX_LDS int*)(sx + 64);
+    float xo = ninf<float>();
+    int n = 0;
+    for (int x0 = 0; x0 < Cm1; x0 += 64) {
+      const int x = x0 + lane;
+      bool in = false;
+      if (x < Cm1) {
+        const float v = cx.row[x + (x >= blank ? 1 : 0)];
+        in = key(v) >= tau;
+        if (!in) xo = v > xo ? v : xo;
+      }
+      const uint64_t m = __ballot(in);
+      if (in) {
+        const int r = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+        sx[n + r] = cx.row[x + (x >= blank ? 1 : 0)];
+        sli[n + r] = x;
+      }
+      n += __builtin_popcountll(m);
+    }
+    xout = uni(wave_max(xo));
+    return n;
+  }
+}
+
 template <typename T, int RN, bool BIG, class SC>
 __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, bool last, int P, int* n_out,
                           int* n_leaves, uint64_t* pc) {
@@ -1293,6 +1378,8 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
   // a closed turn found by the gather, the branch whose children the bitmap holds
   int cqn = 0, cq_i0 = 0, cq_l0 = 0, cbr = -1;
   bool gstop = false;
+  int tsn = -1;      // |S|, the row's top set (row_top_set; -1: not yet computed this frame)
+  T txo = NI;        // the largest value outside S
   while (i0 < nb && !stop) {
     if constexpr (RN == 1 && !BIG && sizeof(T) == 4 && !SC::kStateful) {
       if (st == kTopHeap && W >= 2) {
@@ -1529,6 +1616,9 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       uint64_t hitM = 0, brkM = 0, chM = 0, wkM = 0;
       T otb = NI, ot0 = NI;
       bool enter = true;   // at the gather's start or a branch's first offer
+      if (tsn < 0) tsn = row_top_set(cx, txo);
+      const T tsx = lane < tsn ? (T)row_topx(cx)[lane] : NI;                      // S in label-index order:
+      const int tsl = lane < tsn ? ((CTCX_LDS int*)(row_topx(cx) + 64))[lane] : Cm1;   // lane j its j-th
       while (cqn < 64) {
         if (enter) {
           // the next branch with a turn closed (stop), or with something to
@@ -1573,6 +1663,50 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
           if (res != 0) break;
           enter = false;
           wa0 = -1;
+        }
+        if (tsn > 0 && !(((txo - norm) + ot0) > bottom)) {
+          // every candidate of branch i0 is in S: its offers from li0 on that
+          // beat the bound, merged in label order with its children (from the
+          // bitmap, ascending); a branch that does not fit the chunk's room
+          // starts the next chunk (or, first in the chunk, goes by windows)
+          const bool hot = tsl >= li0 && (((tsx - norm) + ot0) > bottom);
+          const uint64_t hotM = __ballot(hot);
+          const int nh = __builtin_popcountll(hotM);
+          int padd = 0, nch = 0;
+          if (cbr == i0) {
+            for (int q = 0; q * 64 < (Cm1 + 63) / 64; ++q) {
+              uint64_t wq = uni64(cwin[q]);
+              while (wq) {
+                const int a = q * 64 + (int)__builtin_ctzll(wq);
+                wq &= wq - 1ull;
+                uint64_t bits = uni64(cbm[a]);
+                if (a * 64 < li0) bits &= ~lowmask(li0 - a * 64);
+                while (bits) {
+                  const int xc = a * 64 + (int)__builtin_ctzll(bits);
+                  bits &= bits - 1ull;
+                  if (__ballot(hot && tsl == xc)) continue;   // also a hot offer of S
+                  const int pos = cqn + __builtin_popcountll(hotM & __ballot(tsl < xc)) + nch;
+                  if (lane == 0 && pos < 64) cq[pos] = ((uint32_t)i0 << 16) | (uint32_t)xc;
+                  padd += (tsl > xc) ? 1 : 0;
+                  ++nch;
+                }
+              }
+            }
+          }
+          if (nh + nch <= 64 - cqn) {
+            if (hot) {
+              const int r = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(hotM >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((unsigned)hotM, 0u));
+              cq[cqn + r + padd] = ((uint32_t)i0 << 16) | (uint32_t)tsl;
+            }
+            cqn += nh + nch;
+            ++i0;
+            li0 = 0;
+            enter = true;
+            if (i0 >= nb) break;
+            continue;
+          }
+          if (cqn > 0) break;
         }
         // branch i0's aligned 64-label windows from li0 on (lane w: window
         // wa0 + w): one whose labels' block maxima bound every score

@@ -132,9 +132,9 @@ __host__ __device__ inline size_t decode_lds_bytes(int W, int64_t C, int tsize, 
   if (scored) s += a16((2 * (size_t)W + ENC) * tsize); // beam-scorer states (branches x2, entries)
   s += a16((size_t)C * tsize);                  // logit row
   s += a16((size_t)((C + 63) / 64) * tsize);    // its per-64-label block maxima
-  if (C > 64) {                                 // compacted chunk offers, child label bitmap + window summary
+  if (C > 64) {                                 // compacted chunk offers, child label bitmap + window summary, top set
     const size_t nw = (size_t)(C - 1 + 63) / 64;
-    s += 64 * 4 + 8 * nw + 8 * ((nw + 63) / 64);
+    s += 64 * 4 + 8 * nw + 8 * ((nw + 63) / 64) + 64 * 8;   // + the row's top set (value, label index) x 64
   }
   return s;
 }
