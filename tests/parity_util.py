@@ -34,11 +34,11 @@ def compare(out, ref, top_paths, lp_exact=True):
 
 
 def random_case(rng, T_max=40, B_max=3, C_max=11, W_max=15, ties=False, neg_inf=False, dtype=np.float32,
-                C_min=2, scale=1.0):
+                C_min=2, scale=1.0, W_min=1):
     T = int(rng.integers(1, T_max + 1))
     B = int(rng.integers(1, B_max + 1))
     C = int(rng.integers(C_min, C_max + 1))
-    W = int(rng.integers(1, W_max + 1))
+    W = int(rng.integers(W_min, W_max + 1))
     P = int(rng.integers(1, W + 1))
     x = (rng.standard_normal((T, B, C)) * scale).astype(dtype)
     if ties:

@@ -372,6 +372,18 @@ def test_random_large_c_skips():
     _run_random(884, 10, T_max=30, B_max=2, C_min=65, C_max=300, W_max=80, scale=4.0, dtype=np.float64)
 
 
+def test_random_large_c_compacted():
+    # the large-C gather (compacted chunks): wide beams (nb > 64: several
+    # branch groups; W > 128: the RN=2 heap) make most branches parents, so
+    # children are merged into the row's top set or found by the window path;
+    # C near 65 puts nearly every label in the top set; tie-heavy rows put ties
+    # at the top set's threshold; long beams fill chunks mid-branch
+    _run_random(891, 12, T_max=30, B_max=2, C_min=65, C_max=130, W_min=100, W_max=256, scale=1.5)
+    _run_random(892, 12, T_max=30, B_max=2, C_min=65, C_max=70, W_min=30, W_max=128)
+    _run_random(893, 12, T_max=30, B_max=2, C_min=100, C_max=400, W_min=20, W_max=200, ties=True)
+    _run_random(894, 8, T_max=40, B_max=2, C_min=300, C_max=1200, W_min=64, W_max=256, scale=2.5)
+
+
 # ---- large vocabularies (cfg4-like C=1000/W=64, cfg5-like
 # C=5000/W=256), against committed oracle outputs (tests/golden/make_fixtures.py)
 
