@@ -292,11 +292,11 @@ __host__ __device__ void carve(Ctx<T>& cx, CTCX_LDS char* base, int Wcap, int W,
   p += a16(4 * (size_t)cx.hts);
   cx.bloom = (CTCX_LDS uint64_t*)p;
   p += a16(8 * (size_t)Wcap);
-  // TopN elements: positions [0, max(Wcap, 128)] (the mask-form sift reads
-  // child positions up to 128, +inf sentinels past the heap), then one dummy
-  // store slot per lane
+  // TopN elements: positions [0, max(Wcap, 128 or 256)] (the mask-form sift
+  // reads child positions up to 128, or 256 for beams of 129..256, +inf
+  // sentinels past the heap), then one dummy store slot per lane
   cx.he = (CTCX_LDS HE<T>*)p;
-  cx.hdum = (Wcap > 128 ? Wcap : 128) + 2;
+  cx.hdum = (Wcap > 256 ? Wcap : Wcap > 128 ? 256 : 128) + 2;   // the two-node form reads positions up to 256
   p += ((size_t)cx.hdum + 64) * sizeof(HE<T>);
   cx.est[0] = cx.est[1] = cx.eest = nullptr;
   if (scored) {
@@ -751,11 +751,11 @@ __device__ __forceinline__ HeapM heap_m(int dum_base) {
   return g;
 }
 
-// +inf at positions [from, 128] (he[from + 1 .. 129]: every child position a
-// lane can read)
+// +inf at positions [from, to] (to = 128: he[from + 1 .. 129], every child
+// position a lane can read in the one-node-per-lane form; 256 in the two-node form)
 template <typename T>
-__device__ __forceinline__ void heap_sentinels(CTCX_LDS HE<T>* he, int from) {
-  for (int q = from + (int)threadIdx.x; q <= 128; q += 64) he_st(he, q + 1, HE<T>{pinf<T>(), -1});
+__device__ __forceinline__ void heap_sentinels(CTCX_LDS HE<T>* he, int from, int to = 128) {
+  for (int q = from + (int)threadIdx.x; q <= to; q += 64) he_st(he, q + 1, HE<T>{pinf<T>(), -1});
 }
 
 template <typename T>
@@ -789,6 +789,88 @@ __device__ __forceinline__ void push_m(CTCX_LDS HE<T>* he, const HeapM& g, T vv,
   c0 = uni(cv);
   s0 = uni(cs);
   keep = (gt & 1ull) != 0ull;
+}
+
+// The same sift for heaps of 129..256 elements: lane j owns node j (group 0)
+// and node j + 64 (group 1).  Every ancestor of a group-1 node is in group 0
+// (its parent is node 31..63), and every child of a group-1 node is a leaf
+// that is not a lane, so group 1 adds one ballot per predicate and its own
+// pair of stores; the stop is still unique (path nodes are ancestors of one
+// another).  Sentinels at positions [len, 256].
+struct HeapM2 {
+  HeapM g;              // group 0 (the one-node form's geometry)
+  uint64_t anc1, req1;  // node j + 64: its ancestors (all in group 0) and the directions toward it
+};
+
+__device__ __forceinline__ HeapM2 heap_m2(int dum_base) {
+  HeapM2 m;
+  m.g = heap_m(dum_base);
+  uint64_t a[1], r[1];
+  anc_bits_wide<1>(threadIdx.x + 65u, a, r);
+  m.anc1 = a[0];
+  m.req1 = r[0];
+  return m;
+}
+
+template <typename T>
+__device__ __forceinline__ void pairs_m2(const CTCX_LDS HE<T>* he, const HeapM2& g, HE<T> (&L)[2], HE<T> (&R)[2]) {
+  he_ld2(he, g.g.al, L[0], R[0]);
+  he_ld2(he, g.g.al + 128, L[1], R[1]);
+}
+
+template <typename T>
+__device__ __forceinline__ void push_m2(CTCX_LDS HE<T>* he, const HeapM2& g, T vv, int vs, const HE<T> (&L)[2],
+                                        const HE<T> (&R)[2], T& c0, int& s0, bool& keep) {
+  const uint64_t pR0 = __ballot(!(R[0].v > L[0].v)), pR1 = __ballot(!(R[1].v > L[1].v));
+  const bool pr0 = __builtin_amdgcn_inverse_ballot_w64(pR0), pr1 = __builtin_amdgcn_inverse_ballot_w64(pR1);
+  const T cv0 = pr0 ? R[0].v : L[0].v, cv1 = pr1 ? R[1].v : L[1].v;
+  const int cs0 = pr0 ? R[0].s : L[0].s, cs1 = pr1 ? R[1].s : L[1].s;
+  const uint64_t onp0 = __ballot((((unsigned)pR0 ^ g.g.req) & g.g.anc) == 0u);
+  const uint64_t onp1 = __ballot(((pR0 ^ g.req1) & g.anc1) == 0ull);
+  const uint64_t gt0 = __ballot(cv0 > vv), gt1 = __ballot(cv1 > vv);
+  // group 0's one child that is not a lane: node 63's right child (position 128)
+  const uint64_t cnd0 = gt0 | (pR0 & 0x8000000000000000ull);
+  const uint64_t cm0 = onp0 & cnd0;
+  const uint64_t live0 = onp0 & ~__ballot((((unsigned)cm0) & g.g.anc) != 0u);
+  const uint64_t live1 = onp1 & ~__ballot((cm0 & g.anc1) != 0ull);
+  const bool up0 = __builtin_amdgcn_inverse_ballot_w64(live0 & ~gt0);
+  const bool isk0 = __builtin_amdgcn_inverse_ballot_w64(live0 & cnd0);
+  const bool vg0 = __builtin_amdgcn_inverse_ballot_w64(gt0);
+  const bool up1 = __builtin_amdgcn_inverse_ballot_w64(live1 & ~gt1);
+  const bool isk1 = __builtin_amdgcn_inverse_ballot_w64(live1);
+  const bool vg1 = __builtin_amdgcn_inverse_ballot_w64(gt1);
+  he_st(he, up0 ? g.g.aj : g.g.dum, HE<T>{cv0, cs0});
+  he_st(he, isk0 ? (vg0 ? g.g.aj : (pr0 ? g.g.ar : g.g.al)) : g.g.dum, HE<T>{vv, vs});
+  he_st(he, up1 ? g.g.aj + 64 : g.g.dum, HE<T>{cv1, cs1});
+  he_st(he, isk1 ? (vg1 ? g.g.aj + 64 : (pr1 ? g.g.ar + 128 : g.g.al + 128)) : g.g.dum, HE<T>{vv, vs});
+  c0 = uni(cv0);
+  s0 = uni(cs0);
+  keep = (gt0 & 1ull) != 0ull;
+}
+
+// The mask-form sift for RN = 1 (one node per lane) or 2 (two), one interface.
+template <int RN> struct MaskGeo { using type = HeapM; };
+template <> struct MaskGeo<2> { using type = HeapM2; };
+template <int RN>
+__device__ __forceinline__ typename MaskGeo<RN>::type mask_geo(int dum_base) {
+  if constexpr (RN == 2) return heap_m2(dum_base);
+  else return heap_m(dum_base);
+}
+template <typename T, int RN>
+struct MPairs {
+  HE<T> L[RN == 2 ? 2 : 1], R[RN == 2 ? 2 : 1];
+};
+template <typename T, int RN>
+__device__ __forceinline__ void mpairs(const CTCX_LDS HE<T>* he, const typename MaskGeo<RN>::type& g,
+                                       MPairs<T, RN>& p) {
+  if constexpr (RN == 2) pairs_m2(he, g, p.L, p.R);
+  else pairs_m(he, g, p.L[0], p.R[0]);
+}
+template <typename T, int RN>
+__device__ __forceinline__ void mpush(CTCX_LDS HE<T>* he, const typename MaskGeo<RN>::type& g, T vv, int vs,
+                                      const MPairs<T, RN>& p, T& c0, int& s0, bool& keep) {
+  if constexpr (RN == 2) push_m2(he, g, vv, vs, p.L, p.R, c0, s0, keep);
+  else push_m<T>(he, g, vv, vs, p.L[0], p.R[0], c0, s0, keep);
 }
 
 // The HEAP_SORTED event loop for float beams of up to 128 (exact_step), as one
@@ -1889,7 +1971,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     int nev = 0;
     uint64_t done = 0;
     while (true) {
-      if (RN == 1 && st == kTopHeap && W >= 2) {
+      if ((RN == 1 || RN == 2) && st == kTopHeap && W >= 2) {
         // HEAP_SORTED, beams up to 128 (the mask form of the loop below, same
         // decisions): new-child lanes wanting in (NC: live, not a branch) are
         // accepted while they beat the front, re-offers of evicted branch
@@ -1902,12 +1984,12 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
         // frame, so live / cev are not needed after this loop.
         const uint64_t liveM = __ballot(live);
         uint64_t NC = liveM & ~isbm, LB = liveM & isbm, RB = LB & __ballot(cev);
-        const HeapM geo = heap_m(cx.hdum);
+        const auto geo = mask_geo<RN>(cx.hdum);
         T fv = front.v;
         int fs = front.s;
         int nfree = nextfree;
         int nv = uni(nev);
-        if constexpr (sizeof(T) == 4) {
+        if constexpr (sizeof(T) == 4 && RN == 1) {
           // float: the hand-scheduled loop; re-offers of branch children come
           // back here one at a time
           const unsigned heb = (unsigned)(uintptr_t)he;   // LDS byte address of he[0]
@@ -1967,8 +2049,8 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
           for (;;) {
             // the push's child pairs first: they depend only on the previous
             // push's stores, and their latency overlaps the selection below
-            HE<T> pL, pR;
-            pairs_m(he, geo, pL, pR);
+            MPairs<T, RN> pp;
+            mpairs<T, RN>(he, geo, pp);
             const uint64_t gtM = __ballot(s > fv);
             const uint64_t m = ((gtM & NC) | RB) & ~done;
             if (m == 0) break;
@@ -2020,7 +2102,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
             T c0;
             int s0;
             bool keep;
-            push_m<T>(he, geo, k_s, slot, pL, pR, c0, s0, keep);   // push = pop_heap(W + 1)
+            mpush<T, RN>(he, geo, k_s, slot, pp, c0, s0, keep);   // push = pop_heap(W + 1)
             fv = uni(keep ? k_s : c0);
             fs = uni(keep ? slot : s0);
             bat = (sl > k) ? fv : bat;
@@ -2098,7 +2180,10 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
           bat = (sl > k) ? fv : bat;
 #ifdef CTCX_FASTLOOP_PROF
           const uint64_t q3 = __builtin_amdgcn_s_memtime();
-          if (pc) { pc[10] += q1 - q0; pc[12] += q2 - q1; pc[13] += q3 - q2; pc[6] += 1; }
+          if (pc) { pc[10] += q1 - q0; pc[12] += q2 - q1; pc[13] += q3 - q2; }
+#endif
+#ifdef CTCX_PHASES
+          if (pc) pc[6] += 1;
 #endif
         }
         front.v = uni(fv);
@@ -2153,7 +2238,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
             const HE<T> r0 = he_ld(he, 1);
             front = wave_adjust_heap<T, RN>(he, heap_geo<RN>(W, cx.hdum), nv, W);   // pop_heap(W + 1)
             if (lane == 0) he_st(he, W + 1, r0);
-            if (RN == 1 && W >= 2) heap_sentinels(he, W);   // the mask-form sift's geometry
+            if ((RN == 1 || RN == 2) && W >= 2) heap_sentinels(he, W, RN == 2 ? 256 : 128);   // the mask-form sift's geometry
             st = kTopHeap;
 #ifdef CTCX_FASTLOOP_PROF
             if (pc) pc[14] += __builtin_amdgcn_s_memtime() - q4;
@@ -2261,6 +2346,35 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     nout = W;
     if (lane < nout) cx.sorted[lane] = srt0;
     if (lane + 64 < nout) cx.sorted[lane + 64] = srt1;
+  } else if (RN == 2 && st == kTopHeap) {
+    // sort_heap in the two-node mask form (beams 129..256), positions into
+    // register lanes as above (position p: lane p & 63 of srt[p >> 6])
+    const auto geo = mask_geo<RN>(cx.hdum);
+    int fs = uni(front.s);
+    int srt0 = 0, srt1 = 0, srt2 = 0, srt3 = 0;
+    for (int len = W; len > 2; --len) {
+      const HE<T> v = he_ld(he, len);   // e[len-1] (uniform address)
+      if (lane == 0) he_st(he, len, HE<T>{pinf<T>(), -1});   // vacated: a sentinel for the sift over len - 1
+      MPairs<T, RN> pp;
+      mpairs<T, RN>(he, geo, pp);
+      const int pos = len - 1;
+      if (pos >= 192) srt3 = writelane(srt3, fs, pos - 192);
+      else if (pos >= 128) srt2 = writelane(srt2, fs, pos - 128);
+      else if (pos >= 64) srt1 = writelane(srt1, fs, pos - 64);
+      else srt0 = writelane(srt0, fs, pos);
+      T c0;
+      int s0;
+      bool keep;
+      mpush<T, RN>(he, geo, v.v, v.s, pp, c0, s0, keep);
+      fs = keep ? uni(v.s) : s0;
+    }
+    srt0 = writelane(srt0, fs, 1);
+    srt0 = writelane(srt0, uni(he_ld(he, 2).s), 0);
+    nout = W;
+    if (lane < nout) cx.sorted[lane] = srt0;
+    if (lane + 64 < nout) cx.sorted[lane + 64] = srt1;
+    if (lane + 128 < nout) cx.sorted[lane + 128] = srt2;
+    if (lane + 192 < nout) cx.sorted[lane + 192] = srt3;
   } else if (st == kTopHeap) {
     // pop_heap(len): e[len-1] <- e[0], then sift the old e[len-1] from the root
     T fv = front.v;

@@ -128,7 +128,7 @@ __host__ __device__ inline size_t decode_lds_bytes(int W, int64_t C, int tsize, 
   s += 2 * 4 * (size_t)W * 8;                   // prefix hashes, 2 buffers
   s += a16(4 * (size_t)htab_size(W));           // per-frame new-leaf hash table
   s += a16(8 * (size_t)W);                      // per-branch evicted-child label bloom
-  s += ((size_t)(W > 128 ? W : 128) + 2 + 64) * (tsize == 8 ? 16 : 8); // TopN elements (value, slot) + per-lane dummy slots
+  s += ((size_t)(W > 256 ? W : W > 128 ? 256 : 128) + 2 + 64) * (tsize == 8 ? 16 : 8); // TopN elements (value, slot) + per-lane dummy slots
   if (scored) s += a16((2 * (size_t)W + ENC) * tsize); // beam-scorer states (branches x2, entries)
   s += a16((size_t)C * tsize);                  // logit row
   s += a16((size_t)((C + 63) / 64) * tsize);    // its per-64-label block maxima
