@@ -5,8 +5,10 @@
 //   BeamEntry / TopN / LogSumExp             (util/ctc_beam_entry.h, util/ctc_loss_util.h)
 //
 // Kernels (launch order; DESIGN.md has the roofline of each):
-//   ctcx_row_norm     one thread per (t, b) row: softmax normaliser, sequential
-//                     glibc-exact expf sum (decoder.h:72-80).
+//   ctcx_row_norm     one wave per 64 (t, b) rows, staged through LDS in 64-class
+//                     tiles (coalesced loads); one thread per row then sums in
+//                     class order: softmax normaliser, glibc-exact expf sum
+//                     (decoder.h:72-80).
 //   ctcx_beam_decode  one wave64 workgroup per batch item, persistent over t.
 //                     Beam state lives in LDS; per frame it writes one 8-byte
 //                     record per surviving beam (prefix back-link + alignment
