@@ -1005,6 +1005,144 @@ __device__ __forceinline__ int heap_events_f32(float s, int c, int sl, unsigned 
   return st;
 }
 
+// heap_events_f32 for beams of 129..256 (the push_m2 sift: lane j owns node j,
+// group 0, and node j + 64, group 1).  Group 1 adds a second child-pair read
+// (offset 1024 B), its own min-child pick, path test (its ancestors are all in
+// group 0, so the test reads group 0's pick mask), gt and pair of stores.  The
+// stop is the shallowest group-0 path node meeting its stop condition (gt, or
+// node 63's min child being position 128, not a lane); when there is none the
+// path's group-1 node is the stop (its children are never lanes).  The stop
+// mask is live0 & cnd0, which is empty then (s_ff1 gives -1: -2 << 63 = 0).
+// Temporaries: s84..s99, vcc, three compiler-chosen SGPR pairs (p1: group 1's
+// pick, g1: its gt, o1: its path, then live1), v232..v253 (clobbered).
+__device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsigned anc, unsigned req, unsigned an1l,
+                                                  unsigned an1h, unsigned rq1l, unsigned rq1h, unsigned aj,
+                                                  unsigned al, unsigned ar, unsigned aj1, unsigned al1, unsigned ar1,
+                                                  unsigned dum, int& myslot, int& evr, float& bat, uint64_t& NC,
+                                                  uint64_t& RB, uint64_t& done, uint64_t LB, float& fv, int& fs,
+                                                  int& nfree, int& nv, int nb, int& k, int& cnt) {
+  int st;
+  uint64_t p1, g1, o1;
+  const uint64_t k63 = 0x8000000000000000ull;
+  NC = uni64(NC); RB = uni64(RB); done = uni64(done); LB = uni64(LB);
+  fv = uni(fv); fs = uni(fs); nfree = uni(nfree); nv = uni(nv); nb = uni(nb); cnt = uni(cnt);
+  asm volatile(
+      "s_mov_b32 %[st], 0\n\t"
+      "v_cmp_lt_f32_e64 s[88:89], %[fv], %[s]\n\t"          // s > front
+      "s_and_b64 s[88:89], s[88:89], %[nc]\n\t"
+      "s_or_b64 s[88:89], s[88:89], %[rb]\n\t"
+      "s_andn2_b64 s[88:89], s[88:89], %[done]\n\t"        // m (SCC: m != 0)
+      "s_cbranch_scc0 .Lem_exit_%=\n\t"
+      "s_ff1_i32_b64 %[k], s[88:89]\n\t"
+      "s_bitcmp1_b64 %[lb], %[k]\n\t"
+      "s_cbranch_scc1 .Lem_rare_%=\n\t"
+      "ds_read_b128 v[232:235], %[al]\n\t"                 // group 0 child pairs
+      "ds_read_b128 v[244:247], %[al] offset:1024\n\t"     // group 1 child pairs
+      "s_branch .Lem_tail_%=\n"
+      ".Lem_loop_%=:\n\t"
+      CTCX_EVCNT
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "v_cmp_ngt_f32_e64 s[92:93], v234, v232\n\t"         // pR0 = !(R > L)
+      "v_cmp_ngt_f32_e64 %[p1], v246, v244\n\t"            // pR1
+      "v_mov_b32_e32 v240, s84\n\t"
+      "v_mov_b32_e32 v241, s85\n\t"
+      "v_cndmask_b32_e64 v237, v232, v234, s[92:93]\n\t"   // cv0
+      "v_cndmask_b32_e64 v238, v233, v235, s[92:93]\n\t"   // cs0
+      "v_xor_b32_e32 v239, s92, %[req]\n\t"
+      "v_cmp_lt_f32_e64 s[96:97], s84, v237\n\t"           // gt0
+      "v_and_b32_e32 v239, v239, %[anc]\n\t"
+      "v_readfirstlane_b32 s86, v237\n\t"                  // c0: the root's min child
+      "v_cmp_eq_u32_e64 s[94:95], 0, v239\n\t"             // onp0
+      "v_readfirstlane_b32 s87, v238\n\t"
+      "v_xor_b32_e32 v248, s92, %[rq1l]\n\t"
+      "v_xor_b32_e32 v249, s93, %[rq1h]\n\t"
+      "v_and_b32_e32 v248, v248, %[an1l]\n\t"
+      "v_and_b32_e32 v249, v249, %[an1h]\n\t"
+      "v_or_b32_e32 v248, v248, v249\n\t"
+      "v_cndmask_b32_e64 v250, v244, v246, %[p1]\n\t"      // cv1
+      "v_cndmask_b32_e64 v251, v245, v247, %[p1]\n\t"      // cs1
+      "v_cmp_eq_u32_e64 %[o1], 0, v248\n\t"                // onp1
+      "v_cmp_lt_f32_e64 %[g1], s84, v250\n\t"              // gt1
+      "s_and_b64 s[98:99], s[92:93], %[k63]\n\t"
+      "s_or_b64 s[98:99], s[98:99], s[96:97]\n\t"          // cnd0
+      "s_bitcmp1_b32 s96, 0\n\t"                           // keep: v stays at the root
+      "s_cselect_b32 %[fv], s84, s86\n\t"                  // the new front
+      "s_cselect_b32 %[fs], s85, s87\n\t"
+      "v_cmp_lt_i32_e64 vcc, %[k], %[sl]\n\t"              // turns starting after lane k see the new bottom
+      "v_cmp_lt_f32_e64 s[88:89], %[fv], %[s]\n\t"         // next: s > front
+      "s_and_b64 s[90:91], s[94:95], s[98:99]\n\t"         // cm0
+      "s_cmp_eq_u64 s[90:91], 0\n\t"
+      "s_cselect_b64 %[o1], %[o1], 0\n\t"                  // live1: the path's group-1 node, when group 0 has no stop
+      "s_ff1_i32_b64 s86, s[90:91]\n\t"                    // the stop (-1: in group 1)
+      "v_mov_b32_e32 v242, %[fv]\n\t"
+      "s_lshl_b64 s[90:91], -2, s86\n\t"
+      "s_andn2_b64 s[94:95], s[94:95], s[90:91]\n\t"       // live0
+      "s_andn2_b64 s[90:91], s[94:95], s[96:97]\n\t"       // up0
+      "s_and_b64 s[94:95], s[94:95], s[98:99]\n\t"         // stop0 = live0 & cnd0
+      "v_cndmask_b32_e32 %[bat], %[bat], v242, vcc\n\t"
+      "v_cndmask_b32_e64 v236, %[al], %[ar], s[92:93]\n\t"
+      "v_cndmask_b32_e64 v239, %[dum], %[aj], s[90:91]\n\t"
+      "v_cndmask_b32_e64 v236, v236, %[aj], s[96:97]\n\t"  // v lands on the stop (gt) or its min child
+      "ds_write2_b32 v239, v237, v238 offset1:1\n\t"
+      "v_cndmask_b32_e64 v236, %[dum], v236, s[94:95]\n\t"
+      "s_andn2_b64 s[90:91], %[o1], %[g1]\n\t"             // up1
+      "v_cndmask_b32_e64 v253, %[al1], %[ar1], %[p1]\n\t"
+      "ds_write2_b32 v236, v240, v241 offset1:1\n\t"
+      "v_cndmask_b32_e64 v253, v253, %[aj1], %[g1]\n\t"
+      "v_cndmask_b32_e64 v252, %[dum], %[aj1], s[90:91]\n\t"
+      "v_cndmask_b32_e64 v253, %[dum], v253, %[o1]\n\t"    // group 1's stop is its live node
+      "ds_write2_b32 v252, v250, v251 offset1:1\n\t"
+      "s_and_b64 s[88:89], s[88:89], %[nc]\n\t"
+      "s_or_b64 s[88:89], s[88:89], %[rb]\n\t"
+      "ds_write2_b32 v253, v240, v241 offset1:1\n\t"
+      "ds_read_b128 v[232:235], %[al]\n\t"                 // the next push's child pairs
+      "ds_read_b128 v[244:247], %[al] offset:1024\n\t"
+      "s_andn2_b64 s[88:89], s[88:89], %[done]\n\t"        // next m
+      "s_cbranch_scc0 .Lem_exit_%=\n\t"
+      "s_ff1_i32_b64 %[k], s[88:89]\n\t"
+      "s_bitcmp1_b64 %[lb], %[k]\n\t"
+      "s_cbranch_scc1 .Lem_rare_%=\n"
+      ".Lem_tail_%=:\n\t"
+      "s_lshl_b64 s[90:91], -2, %[k]\n\t"
+      "s_not_b64 %[done], s[90:91]\n\t"                    // done = lanes <= k
+      "v_readlane_b32 s84, %[s], %[k]\n\t"                 // v = offer k's score
+      "s_mov_b32 s85, %[fs]\n\t"                           // slot = the front's
+      "s_cmp_lt_i32 %[fs], %[nb]\n\t"
+      "s_cbranch_scc1 .Lem_evb_%=\n"
+      ".Lem_slot_%=:\n\t"
+      "v_cmp_eq_u32_e64 s[90:91], %[fs], %[my]\n\t"        // an entry accepted in this chunk is the evicted front
+      "s_lshl_b64 vcc, 1, %[k]\n\t"
+      "v_mov_b32_e32 v243, s85\n\t"
+      "v_cndmask_b32_e64 %[my], %[my], -1, s[90:91]\n\t"
+      "v_cndmask_b32_e32 %[my], %[my], v243, vcc\n\t"      // lane k: its entry's slot
+      "s_branch .Lem_loop_%=\n"
+      ".Lem_evb_%=:\n\t"
+      "s_mov_b32 s85, %[nfree]\n\t"
+      "s_add_u32 %[nfree], %[nfree], 1\n\t"
+      "s_lshl_b64 s[90:91], 1, %[nv]\n\t"
+      "v_mov_b32_e32 v243, %[fs]\n\t"
+      "s_add_u32 %[nv], %[nv], 1\n\t"
+      "v_cndmask_b32_e64 %[evr], %[evr], v243, s[90:91]\n\t"
+      "v_cmp_eq_u32_e64 s[90:91], %[fs], %[c]\n\t"
+      "s_and_b64 s[90:91], s[90:91], %[lb]\n\t"
+      "s_or_b64 %[rb], %[rb], s[90:91]\n\t"
+      "s_branch .Lem_slot_%=\n"
+      ".Lem_rare_%=:\n\t"
+      "s_mov_b32 %[st], 1\n"
+      ".Lem_exit_%=:\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : [my] "+v"(myslot), [evr] "+v"(evr), [bat] "+v"(bat), [nc] "+s"(NC), [rb] "+s"(RB), [done] "+s"(done),
+        [fv] "+s"(fv), [fs] "+s"(fs), [nfree] "+s"(nfree), [nv] "+s"(nv), [k] "=&s"(k), [st] "=&s"(st),
+        [cnt] "+s"(cnt), [p1] "=&s"(p1), [g1] "=&s"(g1), [o1] "=&s"(o1)
+      : [s] "v"(s), [c] "v"(c), [sl] "v"(sl), [anc] "v"(anc), [req] "v"(req), [an1l] "v"(an1l), [an1h] "v"(an1h),
+        [rq1l] "v"(rq1l), [rq1h] "v"(rq1h), [aj] "v"(aj), [al] "v"(al), [ar] "v"(ar), [aj1] "v"(aj1),
+        [al1] "v"(al1), [ar1] "v"(ar1), [dum] "v"(dum), [lb] "s"(LB), [nb] "s"(nb), [k63] "s"(k63)
+      : "memory", "vcc", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96",
+        "s97", "s98", "s99", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239", "v240", "v241",
+        "v242", "v243", "v244", "v245", "v246", "v247", "v248", "v249", "v250", "v251", "v252", "v253");
+  return st;
+}
+
 // The same event loop over one half of a 128-offer window (exact_step's
 // window path): the current half's offers are s/c/sl/myslot/bat and its lane
 // masks, the other half's appear only in the bookkeeping -- an evicted front
@@ -1991,7 +2129,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
         int fs = front.s;
         int nfree = nextfree;
         int nv = uni(nev);
-        if constexpr (sizeof(T) == 4 && RN == 1) {
+        if constexpr (sizeof(T) == 4 && (RN == 1 || RN == 2)) {
           // float: the hand-scheduled loop; re-offers of branch children come
           // back here one at a time
           const unsigned heb = (unsigned)(uintptr_t)he;   // LDS byte address of he[0]
@@ -2002,8 +2140,16 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
             fv = uni(fv); fs = uni(fs); nfree = uni(nfree); nv = uni(nv);
             int nev_asm = 0;
             const uint64_t ta = pc ? __builtin_amdgcn_s_memtime() : 0;
-            const int est = heap_events_f32(s, c, sl, geo.anc, geo.req, aj, al, ar, dum, myslot, evr, bat, NC, RB, done,
-                                            LB, fv, fs, nfree, nv, uni(nb), k, nev_asm);
+            int est;
+            if constexpr (RN == 1) {
+              est = heap_events_f32(s, c, sl, geo.anc, geo.req, aj, al, ar, dum, myslot, evr, bat, NC, RB, done, LB,
+                                    fv, fs, nfree, nv, uni(nb), k, nev_asm);
+            } else {
+              est = heap_events_m2_f32(s, c, sl, geo.g.anc, geo.g.req, (unsigned)geo.anc1, (unsigned)(geo.anc1 >> 32),
+                                       (unsigned)geo.req1, (unsigned)(geo.req1 >> 32), aj, al, ar, aj + 512u,
+                                       al + 1024u, ar + 1024u, dum, myslot, evr, bat, NC, RB, done, LB, fv, fs,
+                                       nfree, nv, nb, k, nev_asm);
+            }
             if (pc) { pc[13] += __builtin_amdgcn_s_memtime() - ta; pc[6] += uni(nev_asm); pc[12] += 1; }
             if (est == 0) break;
             k = uni(k);
@@ -2037,12 +2183,12 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
             const T k_s = bcast(s, k);
             myslot = (myslot == fs) ? -1 : myslot;
             myslot = __builtin_amdgcn_inverse_ballot_w64(1ull << k) ? kc : myslot;
-            HE<T> pL, pR;
-            pairs_m(he, geo, pL, pR);
+            MPairs<T, RN> pp;
+            mpairs<T, RN>(he, geo, pp);
             T c0;
             int s0;
             bool keep;
-            push_m<T>(he, geo, k_s, kc, pL, pR, c0, s0, keep);
+            mpush<T, RN>(he, geo, k_s, kc, pp, c0, s0, keep);
             fv = keep ? k_s : c0;
             fs = keep ? kc : s0;
             bat = (sl > k) ? fv : bat;
