@@ -905,6 +905,9 @@ __device__ __forceinline__ int heap_events_f32(float s, int c, int sl, unsigned 
                                                float& fv, int& fs, int& nfree, int& nv, int nb, int& k, int& cnt) {
   int st;
   const uint64_t k31 = 0x80000000ull, khi = 0xffffffff00000000ull;
+  // every scalar operand provably uniform (the asm's "s" constraints)
+  NC = uni64(NC); RB = uni64(RB); done = uni64(done); LB = uni64(LB);
+  fv = uni(fv); fs = uni(fs); nfree = uni(nfree); nv = uni(nv); nb = uni(nb); cnt = uni(cnt);
   asm volatile(
       "s_mov_b32 %[st], 0\n\t"
       // select the first event
@@ -1283,6 +1286,8 @@ __device__ __forceinline__ int heap_events2_f32(float s, int c, int sl, int co, 
 __device__ __forceinline__ void extract_f32(unsigned heb, int hi, int lo, int base, unsigned anc, unsigned req,
                                             unsigned aj, unsigned al, unsigned ar, unsigned dum, int& srt, int& fs) {
   const uint64_t k31 = 0x80000000ull, khi = 0xffffffff00000000ull;
+  // every scalar operand provably uniform (the asm's "s" constraints)
+  heb = (unsigned)uni((int)heb); hi = uni(hi); lo = uni(lo); base = uni(base); fs = uni(fs);
   asm volatile(
       "s_mov_b32 s84, %[hi]\n\t"
       "s_mov_b64 s[90:91], 1\n\t"                          // lane 0
@@ -1440,29 +1445,54 @@ __device__ __forceinline__ int row_top_set(const Ctx<T>& cx, T& xout) {
     constexpr int KR = 16;   // rows of up to 64 * KR labels keep their keys in registers
     unsigned kr[KR];
     const bool inreg = Cm1 <= 64 * KR;
+    unsigned lmax = 0u, lmaxx = 0u;   // the lane's largest key (rows > 64 * KR: over its stripe)
 #pragma unroll
     for (int j = 0; j < KR; ++j) {
       const int x = 64 * j + lane;
       kr[j] = (inreg && x < Cm1) ? kat(x) : 0u;
+      lmax = kr[j] > lmax ? kr[j] : lmax;
     }
+    if (!inreg) {
+#pragma unroll 8
+      for (int x = lane; x < Cm1; x += 64) {
+        const unsigned kx = kat(x);
+        lmaxx = kx > lmaxx ? kx : lmaxx;
+      }
+      lmax = lmaxx;
+    }
+    // |{key >= tau}|: each lane counts its own labels (no ballot per 64
+    // labels), then one bit-sliced wave sum (a lane counts at most 1024)
+    const int nbits = 32 - __builtin_clz((unsigned)((Cm1 + 63) / 64));
     auto cnt_ge = [&](unsigned tau) {
       int c = 0;
       if (inreg) {
 #pragma unroll
-        for (int j = 0; j < KR; ++j) {
-          const int x = 64 * j + lane;
-          c += __builtin_popcountll(__ballot(x < Cm1 && kr[j] >= tau));
-        }
+        for (int j = 0; j < KR; ++j) c += (kr[j] >= tau && 64 * j + lane < Cm1) ? 1 : 0;
       } else {
-        for (int x0 = 0; x0 < Cm1; x0 += 64) {
-          const int x = x0 + lane;
-          c += __builtin_popcountll(__ballot(x < Cm1 && kat(x) >= tau));
-        }
+#pragma unroll 8
+        for (int x = lane; x < Cm1; x += 64) c += (kat(x) >= tau) ? 1 : 0;
       }
-      return c;
+      int tot = 0;
+      for (int b = 0; b < nbits; ++b) tot += __builtin_popcountll(__ballot((c >> b) & 1)) << b;
+      return tot;
     };
-    // smallest tau with |{key >= tau}| <= 64: cnt(lo) > 64 >= cnt(hi)
+    // smallest tau with |{key >= tau}| <= 64: cnt(lo) > 64 >= cnt(hi).  The
+    // answer's set S is that of the row's 64 largest values without a tie
+    // across the boundary, so any bracket with the invariant gives the same S.
+    // Bracket: hi = the row's largest key + 1; the smallest lane maximum km has
+    // at least 64 keys at or above it (one per lane), so cnt(km) >= 64: either
+    // exactly the 64 largest, or lo = km
     uint64_t lo = 0, hi = 1ull << 32;
+    if (Cm1 <= 64) {
+      hi = 0;
+    } else {
+      hi = (uint64_t)(unsigned)uni((int)wave_max(lmax)) + 1ull;
+      const unsigned km = (unsigned)uni((int)wave_min(lmax));
+      const int c = cnt_ge(km);
+      if (c > 64) lo = km;
+      else hi = km;
+      if (c == 64) lo = hi;   // exactly the 64 largest
+    }
     while (hi - lo > 1) {
       const uint64_t mid = (lo + hi) >> 1;
       const int c = cnt_ge((unsigned)mid);

@@ -1,0 +1,4 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 900 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/ > gpurun_out/gputest.log 2>&1 || { echo "pytest rc=$?" >> gpurun_out/gputest.log; exit 1; }
+TAG=r2f bash tools/profile_round.sh
