@@ -1349,6 +1349,104 @@ __device__ __forceinline__ void extract_f32(unsigned heb, int hi, int lo, int ba
         "v243", "v244", "v245", "v246", "v247", "v248", "v249", "v250", "v251");
 }
 
+// extract_f32 over the two-group heap (beams 129..256: the push_m2 sift), for
+// pops that leave more than 128 elements (len > 129); below that the heap
+// fits the one-group form and extract_f32 takes over on the same layout (the
+// vacated positions up to 256 hold sentinels).  Group 1's pick, path test
+// (against group 0's pick mask), gt and stores as in heap_events_m2_f32.
+// Temporaries: s84..s99, v232..v255 (clobbered) and compiler-chosen registers
+// (p1, g1, o1: SGPR pairs; t0, t1, c1v, c1s, a1, u1: VGPRs, the last four DS
+// operands, rewritten only after the s_waitcnt that retires them).
+__device__ __forceinline__ void extract_m2_f32(unsigned heb, int hi, int lo, int base, unsigned anc, unsigned req,
+                                               unsigned an1l, unsigned an1h, unsigned rq1l, unsigned rq1h,
+                                               unsigned aj, unsigned al, unsigned ar, unsigned aj1, unsigned al1,
+                                               unsigned ar1, unsigned dum, int& srt, int& fs) {
+  const uint64_t k63 = 0x8000000000000000ull;
+  uint64_t p1, g1, o1;
+  unsigned t0, t1, c1v, c1s, a1, u1;
+  heb = (unsigned)uni((int)heb); hi = uni(hi); lo = uni(lo); base = uni(base); fs = uni(fs);
+  asm volatile(
+      "s_mov_b32 s84, %[hi]\n\t"
+      "s_mov_b64 s[90:91], 1\n\t"                          // lane 0
+      "v_mov_b32_e32 v242, 0x7f800000\n\t"                 // the sentinel (+inf, -1)
+      "v_mov_b32_e32 v243, -1\n"
+      ".Ly_top_%=:\n\t"
+      "s_cmp_le_i32 s84, %[lo]\n\t"
+      "s_cbranch_scc1 .Ly_end_%=\n\t"
+      "s_lshl_b32 s85, s84, 3\n\t"
+      "s_add_u32 s85, s85, %[heb]\n\t"                     // he[len]: position len - 1
+      "s_sub_u32 s86, s84, 1\n\t"
+      "s_sub_u32 s86, s86, %[base]\n\t"
+      "s_lshl_b64 s[88:89], 1, s86\n\t"                    // its lane in srt
+      "v_mov_b32_e32 v236, s85\n\t"
+      "v_mov_b32_e32 v240, %[fs]\n\t"
+      "ds_read_b64 v[238:239], v236\n\t"                   // e[len - 1] (every lane: broadcast)
+      "v_cndmask_b32_e64 v241, %[dum], v236, s[90:91]\n\t"
+      "v_cndmask_b32_e64 %[srt], %[srt], v240, s[88:89]\n\t"   // the front: position len - 1
+      "ds_write_b64 v241, v[242:243]\n\t"                  // lane 0: the sentinel
+      "ds_read_b128 v[232:235], %[al]\n\t"                 // group 0 child pairs
+      "ds_read_b128 v[252:255], %[al] offset:1024\n\t"     // group 1 child pairs
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "v_cmp_ngt_f32_e64 s[92:93], v234, v232\n\t"         // pR0
+      "v_cmp_ngt_f32_e64 %[p1], v254, v252\n\t"            // pR1
+      "v_mov_b32_e32 v244, v238\n\t"
+      "v_mov_b32_e32 v245, v239\n\t"
+      "v_cndmask_b32_e64 v248, v232, v234, s[92:93]\n\t"   // cv0
+      "v_cndmask_b32_e64 v249, v233, v235, s[92:93]\n\t"   // cs0
+      "v_xor_b32_e32 v251, s92, %[req]\n\t"
+      "v_cmp_lt_f32_e64 s[96:97], v238, v248\n\t"          // gt0: min child > v
+      "v_and_b32_e32 v251, v251, %[anc]\n\t"
+      "v_readfirstlane_b32 s87, v239\n\t"                  // v's slot
+      "v_cmp_eq_u32_e64 s[94:95], 0, v251\n\t"             // onp0
+      "v_readfirstlane_b32 s86, v249\n\t"                  // s0
+      "v_xor_b32_e32 %[t0], s92, %[rq1l]\n\t"
+      "v_xor_b32_e32 %[t1], s93, %[rq1h]\n\t"
+      "v_and_b32_e32 %[t0], %[t0], %[an1l]\n\t"
+      "v_and_b32_e32 %[t1], %[t1], %[an1h]\n\t"
+      "v_or_b32_e32 %[t0], %[t0], %[t1]\n\t"
+      "v_cndmask_b32_e64 %[c1v], v252, v254, %[p1]\n\t"    // cv1
+      "v_cndmask_b32_e64 %[c1s], v253, v255, %[p1]\n\t"    // cs1
+      "v_cmp_eq_u32_e64 %[o1], 0, %[t0]\n\t"               // onp1
+      "v_cmp_lt_f32_e64 %[g1], v238, %[c1v]\n\t"           // gt1
+      "s_and_b64 s[98:99], s[92:93], %[k63]\n\t"
+      "s_or_b64 s[98:99], s[98:99], s[96:97]\n\t"          // cnd0
+      "s_and_b64 s[88:89], s[94:95], s[98:99]\n\t"         // cm0
+      "s_cmp_eq_u64 s[88:89], 0\n\t"
+      "s_cselect_b64 %[o1], %[o1], 0\n\t"                  // live1
+      "s_ff1_i32_b64 s88, s[88:89]\n\t"                    // the stop (-1: in group 1)
+      "s_lshl_b64 s[88:89], -2, s88\n\t"
+      "s_andn2_b64 s[94:95], s[94:95], s[88:89]\n\t"       // live0
+      "s_andn2_b64 s[88:89], s[94:95], s[96:97]\n\t"       // up0
+      "s_and_b64 s[98:99], s[94:95], s[98:99]\n\t"         // stop0 = live0 & cnd0
+      "v_cndmask_b32_e64 v250, %[al], %[ar], s[92:93]\n\t"
+      "v_cndmask_b32_e64 v247, %[dum], %[aj], s[88:89]\n\t"
+      "v_cndmask_b32_e64 v250, v250, %[aj], s[96:97]\n\t"
+      "ds_write2_b32 v247, v248, v249 offset1:1\n\t"
+      "v_cndmask_b32_e64 v250, %[dum], v250, s[98:99]\n\t"
+      "s_andn2_b64 s[88:89], %[o1], %[g1]\n\t"             // up1
+      "v_cndmask_b32_e64 %[a1], %[al1], %[ar1], %[p1]\n\t"
+      "ds_write2_b32 v250, v244, v245 offset1:1\n\t"
+      "v_cndmask_b32_e64 %[a1], %[a1], %[aj1], %[g1]\n\t"
+      "v_cndmask_b32_e64 %[u1], %[dum], %[aj1], s[88:89]\n\t"
+      "v_cndmask_b32_e64 %[a1], %[dum], %[a1], %[o1]\n\t"  // group 1's stop is its live node
+      "ds_write2_b32 %[u1], %[c1v], %[c1s] offset1:1\n\t"
+      "ds_write2_b32 %[a1], v244, v245 offset1:1\n\t"
+      "s_bitcmp1_b32 s96, 0\n\t"                           // keep: v stays at the root
+      "s_cselect_b32 %[fs], s87, s86\n\t"
+      "s_sub_u32 s84, s84, 1\n\t"
+      "s_branch .Ly_top_%=\n"
+      ".Ly_end_%=:\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : [srt] "+v"(srt), [fs] "+s"(fs), [p1] "=&s"(p1), [g1] "=&s"(g1), [o1] "=&s"(o1), [t0] "=&v"(t0),
+        [t1] "=&v"(t1), [c1v] "=&v"(c1v), [c1s] "=&v"(c1s), [a1] "=&v"(a1), [u1] "=&v"(u1)
+      : [heb] "s"(heb), [hi] "s"(hi), [lo] "s"(lo), [base] "s"(base), [anc] "v"(anc), [req] "v"(req),
+        [an1l] "v"(an1l), [an1h] "v"(an1h), [rq1l] "v"(rq1l), [rq1h] "v"(rq1h), [aj] "v"(aj), [al] "v"(al),
+        [ar] "v"(ar), [aj1] "v"(aj1), [al1] "v"(al1), [ar1] "v"(ar1), [dum] "v"(dum), [k63] "s"(k63)
+      : "memory", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97",
+        "s98", "s99", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239", "v240", "v241", "v242",
+        "v243", "v244", "v245", "v246", "v247", "v248", "v249", "v250", "v251", "v252", "v253", "v254", "v255");
+}
+
 // peek_bottom() in the UNORDERED state: the first minimum moves to the front.
 // Returns the new front.
 template <typename T>
@@ -2530,6 +2628,21 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     const auto geo = mask_geo<RN>(cx.hdum);
     int fs = uni(front.s);
     int srt0 = 0, srt1 = 0, srt2 = 0, srt3 = 0;
+    if constexpr (sizeof(T) == 4 && RN == 2) {
+      const unsigned heb = (unsigned)(uintptr_t)he;
+      const unsigned aj = heb + 8u * (unsigned)(lane + 1), al = heb + 8u * (unsigned)(2 * lane + 2);
+      const unsigned ar = al + 8u, dum = heb + 8u * (unsigned)(cx.hdum + lane);
+      const unsigned an1l = (unsigned)geo.anc1, an1h = (unsigned)(geo.anc1 >> 32);
+      const unsigned rq1l = (unsigned)geo.req1, rq1h = (unsigned)(geo.req1 >> 32);
+      // positions 255..192 into srt3, 191..128 into srt2 (two-group sift),
+      // then 127..64 into srt1 and 63..2 into srt0 (one-group sift)
+      extract_m2_f32(heb, uni(W), 192, 192, geo.g.anc, geo.g.req, an1l, an1h, rq1l, rq1h, aj, al, ar, aj + 512u,
+                     al + 1024u, ar + 1024u, dum, srt3, fs);
+      extract_m2_f32(heb, uni(W < 192 ? W : 192), 128, 128, geo.g.anc, geo.g.req, an1l, an1h, rq1l, rq1h, aj, al,
+                     ar, aj + 512u, al + 1024u, ar + 1024u, dum, srt2, fs);
+      extract_f32(heb, uni(W < 128 ? W : 128), 64, 64, geo.g.anc, geo.g.req, aj, al, ar, dum, srt1, fs);
+      extract_f32(heb, uni(W < 64 ? W : 64), 2, 0, geo.g.anc, geo.g.req, aj, al, ar, dum, srt0, fs);
+    } else
     for (int len = W; len > 2; --len) {
       const HE<T> v = he_ld(he, len);   // e[len-1] (uniform address)
       if (lane == 0) he_st(he, len, HE<T>{pinf<T>(), -1});   // vacated: a sentinel for the sift over len - 1

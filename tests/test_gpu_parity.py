@@ -384,6 +384,16 @@ def test_random_large_c_compacted():
     _run_random(894, 8, T_max=40, B_max=2, C_min=300, C_max=1200, W_min=64, W_max=256, scale=2.5)
 
 
+def test_random_wide_beam_events():
+    # beams of 129..256 (float): the two-group asm event loop (heap_events_m2_f32)
+    # with the stop in either group, small C (64-offer chunks) and large C
+    # (compacted chunks); tie-heavy rows exercise the right-on-ties picks of
+    # both groups and the stop at node 63's right child
+    _run_random(901, 10, T_max=40, B_max=2, C_min=3, C_max=40, W_min=129, W_max=256)
+    _run_random(902, 10, T_max=40, B_max=2, C_min=3, C_max=30, W_min=129, W_max=256, ties=True)
+    _run_random(903, 8, T_max=30, B_max=2, C_min=65, C_max=500, W_min=129, W_max=256, ties=True)
+
+
 # ---- large vocabularies (cfg4-like C=1000/W=64, cfg5-like
 # C=5000/W=256), against committed oracle outputs (tests/golden/make_fixtures.py)
 
