@@ -1966,7 +1966,11 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       uint64_t hitM = 0, brkM = 0, chM = 0, wkM = 0;
       T otb = NI, ot0 = NI;
       bool enter = true;   // at the gather's start or a branch's first offer
-      if (tsn < 0) tsn = row_top_set(cx, txo);
+      const uint64_t tg0 = pc ? __builtin_amdgcn_s_memtime() : 0;
+      if (tsn < 0) {
+        tsn = row_top_set(cx, txo);
+        if (pc) pc[19] += __builtin_amdgcn_s_memtime() - tg0;
+      }
       const T tsx = lane < tsn ? (T)row_topx(cx)[lane] : NI;                      // S in label-index order:
       const int tsl = lane < tsn ? ((CTCX_LDS int*)(row_topx(cx) + 64))[lane] : Cm1;   // lane j its j-th
       while (cqn < 64) {
@@ -2061,6 +2065,8 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
         // branch i0's aligned 64-label windows from li0 on (lane w: window
         // wa0 + w): one whose labels' block maxima bound every score
         // (xb - norm) + ot0 <= bottom and that holds no child is passed over
+        const uint64_t tw0 = pc ? __builtin_amdgcn_s_memtime() : 0;
+        if (pc) pc[17] += 1;
         if (wa0 < 0 || (li0 >> 6) >= wa0 + 64) {
           wa0 = li0 >> 6;
           const int lw = (wa0 + lane) * 64;
@@ -2129,6 +2135,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
           if (nli0 < 0) nli0 = endw;
         }
         li0 = nli0;
+        if (pc) pc[18] += __builtin_amdgcn_s_memtime() - tw0;
         if (li0 >= Cm1) {
           ++i0;
           li0 = 0;
@@ -2136,6 +2143,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
           if (i0 >= nb) break;
         }
       }
+      if (pc) pc[16] += __builtin_amdgcn_s_memtime() - tg0;
       if (cqn == 0) {
         if (gstop) stop = true;
         break;
