@@ -1974,6 +1974,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       const T tsx = lane < tsn ? (T)row_topx(cx)[lane] : NI;                      // S in label-index order:
       const int tsl = lane < tsn ? ((CTCX_LDS int*)(row_topx(cx) + 64))[lane] : Cm1;   // lane j its j-th
       while (cqn < 64) {
+        const uint64_t te0 = pc ? __builtin_amdgcn_s_memtime() : 0;
         if (enter) {
           // the next branch with a turn closed (stop), or with something to
           // gather (pmax + ot > bottom, or children)
@@ -2013,12 +2014,51 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
             }
             break;
           }
+          if (pc) pc[20] += __builtin_amdgcn_s_memtime() - te0;
           if (res == 1) gstop = true;
           if (res != 0) break;
+          if (pc) pc[21] += 1;
           enter = false;
           wa0 = -1;
         }
         if (tsn > 0 && !(((txo - norm) + ot0) > bottom)) {
+          if (pc) pc[22] += 1;
+          if (li0 == 0 && cbr != i0) {
+            // a run of branches i0, i0 + 1, ... (lane L: branch i0 + L) each
+            // with every candidate in S, no branch children and an open turn
+            // (branch i0's was checked by the branch scan): each takes one
+            // ballot of its S offers that beat the bound, in branch order,
+            // while they fit the chunk -- the same decisions and entries as
+            // the per-branch path below, without its branch selection
+            const int ib = i0 + lane;
+            const bool vb = ib < nb;
+            const T otL = vb ? sel(cx.ot, buf)[ib] : NI;
+            const bool okL = vb && (otL > bottom) && cx.head[ib] < 0 && !(((txo - norm) + otL) > bottom);
+            const uint64_t badM = ~__ballot(okL || lane == 0);
+            const int R = badM ? (int)__builtin_ctzll(badM) : 64;   // run length (>= 1)
+            const T sxv = tsx - norm;                                // S lane j: x_j - norm
+            int L = 0;
+            for (; L < R; ++L) {
+              const T ob = bcast(otL, L);
+              const bool h = lane < tsn && ((sxv + ob) > bottom);
+              const uint64_t hM = __ballot(h);
+              const int nh = __builtin_popcountll(hM);
+              if (nh > 64 - cqn) break;
+              if (h) {
+                const int r = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(hM >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((unsigned)hM, 0u));
+                cq[cqn + r] = ((uint32_t)(i0 + L) << 16) | (uint32_t)tsl;
+              }
+              cqn += nh;
+            }
+            if (L > 0) {
+              i0 += L;
+              li0 = 0;
+              enter = true;
+              if (i0 >= nb) break;
+              continue;
+            }
+          }
           // every candidate of branch i0 is in S: its offers from li0 on that
           // beat the bound, merged in label order with its children (from the
           // bitmap, ascending); a branch that does not fit the chunk's room
@@ -2047,6 +2087,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
               }
             }
           }
+          if (pc) pc[23] += __builtin_amdgcn_s_memtime() - te0;
           if (nh + nch <= 64 - cqn) {
             if (hot) {
               const int r = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(hotM >> 32),

@@ -17,16 +17,17 @@ f = _lib.CTCEXT_FLAG_PHASES | _lib.CTCEXT_FLAG_PROFILE
 ctcext_amd.ctc_ext_beam_search_decoder(x, sl, W, P, merge_repeated=True, flags=f)
 out = ctcext_amd.ctc_ext_beam_search_decoder(x, sl, W, P, merge_repeated=True, flags=f)
 d = ctcext_amd.get_decoder(0)
-buf = np.zeros((B, 20), np.uint64)
-d.lib.ctcext_phase_counters(d.handle, ctypes.c_void_p(buf.ctypes.data), B * 20)
+buf = np.zeros((B, 24), np.uint64)
+d.lib.ctcext_phase_counters(d.handle, ctypes.c_void_p(buf.ctypes.data), B * 24)
 m = buf.astype(np.float64).mean(0)
 fr = m[7]
 names = ["rowload", "recursion", "grow", "extract", "commit", "literal", "heap events", "frames",
          "scoring", "eventloop", "score:pre-skip", "chunks", "asm calls", "asm loop", "makeheap", "flush",
-         "gather (C>64)", "gather: window steps", "gather: windows", "gather: top set"]
-CYC = {0, 1, 2, 3, 4, 5, 8, 9, 10, 13, 14, 15, 16, 18, 19}
+         "gather (C>64)", "gather: window steps", "gather: windows", "gather: top set",
+         "gather: branch select", "gather: branches", "gather: S branches", "gather: select+S test+S hot"]
+CYC = {0, 1, 2, 3, 4, 5, 8, 9, 10, 13, 14, 15, 16, 18, 19, 20, 23}
 print("B=%d T=%d W=%d P=%d C=%d decode_ms=%.1f" % (B, T, W, P, C, d.last_stats["decode_kernel_ms"]))
-for k in range(20):
+for k in range(24):
     if k == 7:
         continue
     print("  %-10s %12.0f %s/frame" % (names[k], m[k] / fr, "cycles" if k in CYC else "count"))
