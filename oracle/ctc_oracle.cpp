@@ -40,7 +40,11 @@
 //   kShared:   a candidate is (prob, index into an append-only (label, prev)
 //              arena) and only the first-pushed maximum is kept.  Same results
 //              (only .top() of each queue is ever read, ctc_beam_entry.h:92-99),
-//              O(W*C*T) cost; used for mid-size parity cases.
+//              O(W*C) time per frame.  Nodes that GetChild would create only to
+//              be deactivated are never materialised, and unreachable
+//              never-used nodes are reclaimed (Decoder::reclaim), so memory is
+//              O(live prefixes): full-length cfg4/cfg5 items fit.  This is the
+//              parity checker.
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -137,9 +141,13 @@ struct VecCand {             // reference-shaped candidate (ctc_beam_entry.h:46-
   VecCand() : prob(LogZero<T>()) {}
   VecCand(std::vector<int> s, T p) : prob(p), seq(s) {}   // by value, then copied: as the reference
 };
+// BeamAlignmentCandidateComparer (ctc_beam_entry.h:65-73): virtual, and it
+// takes both candidates BY VALUE, so every heap comparison copies two label
+// sequences.  Kept that way here: it is part of the reference's cost.
 template <class T>
 struct VecCandLess {
-  bool operator()(const VecCand<T>& a, const VecCand<T>& b) const { return a.prob < b.prob; }
+  virtual ~VecCandLess() {}
+  virtual bool operator()(const VecCand<T> a, const VecCand<T> b) const { return a.prob < b.prob; }
 };
 
 template <class T>
@@ -148,9 +156,16 @@ struct FaithfulStore {
   struct Slots { Queue q[2]; };  // [0] = blank-ending, [1] = label-ending
   static bool has(const Slots& s, int k) { return !s.q[k].empty(); }
   static T prob(const Slots& s, int k) { return s.q[k].top().prob; }
-  static void clear(Slots& s) { s.q[0] = Queue(); s.q[1] = Queue(); }
-  // dst gets candidate (base(src,k) + p, base.seq ++ [label])
+  // BeamAlignment::Reset (ctc_beam_entry.h:84-91) pops every element
+  static void clear(Slots& s) {
+    while (!s.q[0].empty()) s.q[0].pop();
+    while (!s.q[1].empty()) s.q[1].pop();
+  }
+  // old_cands = new_cands; new_cands.Reset()   (decoder.h:87-92)
+  static void roll(Slots& old, Slots& nw) { old = nw; clear(nw); }
+  // GetBlank / GetNBlank (ctc_beam_entry.h:92-99): a copy of top()
   static VecCand<T> top_copy(const Queue& q) { VecCand<T> r = q.top(); return r; }
+  static constexpr bool kLazyNodes = false;
   // Same allocation/copy pattern as the reference's AddAlignmentCandidate
   // (ctc_beam_entry.h:190-228), so its O(t) copies per call are reproduced.
   void add(Slots& dst, int to_k, const Slots& src, int from_k, T base_if_none, T p, int label) {
@@ -158,7 +173,7 @@ struct FaithfulStore {
     std::vector<int> old_seq;
     T base;
     if (!src.q[from_k].empty()) {
-      old_cand = top_copy(src.q[from_k]);
+      old_cand = top_copy(src.q[from_k]);   // move-assigned from the returned copy
       base = old_cand.prob;
       old_seq = old_cand.seq;
     } else {
@@ -173,13 +188,38 @@ struct FaithfulStore {
   void reset_all() {}
 };
 
+// Shared store: a candidate is its probability plus a back-link into an
+// append-only (label, prev) arena; only the first-pushed maximum of each kind
+// is kept (only .top() is ever read, ctc_beam_entry.h:92-99).  A candidate
+// of the current frame (new_c) is held unmaterialised as (label, prev) and
+// enters the arena only when its entry rolls it into old_c as a branch
+// (decoder.h:87-92), so the arena grows by <= 2 entries per branch per frame
+// instead of one per AddAlignmentCandidate call: cost only, the candidate
+// sequences are identical.
 template <class T>
 struct SharedStore {
-  struct Slots { T p[2]; int32_t id[2]; bool ok[2]; Slots() { ok[0] = ok[1] = false; } };
+  struct Slots {
+    T p[2];
+    int32_t label[2], prev[2];  // new_c form: appended label, arena id of the source (-1: none)
+    int32_t id[2];              // old_c form: arena id of the whole sequence
+    bool ok[2];
+    Slots() { ok[0] = ok[1] = false; }
+  };
   std::vector<std::pair<int32_t, int32_t>> arena;  // (label, prev id or -1)
+  static constexpr bool kLazyNodes = true;
   static bool has(const Slots& s, int k) { return s.ok[k]; }
   static T prob(const Slots& s, int k) { return s.p[k]; }
   static void clear(Slots& s) { s.ok[0] = s.ok[1] = false; }
+  void roll(Slots& old, Slots& nw) {
+    for (int k = 0; k < 2; ++k) {
+      old.ok[k] = nw.ok[k];
+      if (!nw.ok[k]) continue;
+      arena.emplace_back(nw.label[k], nw.prev[k]);
+      old.p[k] = nw.p[k];
+      old.id[k] = (int32_t)arena.size() - 1;
+    }
+    clear(nw);
+  }
   void add(Slots& dst, int to_k, const Slots& src, int from_k, T base_if_none, T p, int label) {
     T base;
     int32_t prev;
@@ -188,14 +228,16 @@ struct SharedStore {
     const T np = base + p;
     // first-pushed maximum == std::priority_queue::top() under a strict '<'
     if (dst.ok[to_k] && !(np > dst.p[to_k])) return;
-    arena.emplace_back(label, prev);
     dst.p[to_k] = np;
-    dst.id[to_k] = (int32_t)arena.size() - 1;
+    dst.label[to_k] = label;
+    dst.prev[to_k] = prev;
     dst.ok[to_k] = true;
   }
+  // sequence of a new_c candidate (TopPaths reads new_cands, ctc_beam_entry.h:137-152)
   std::vector<int> sequence(const Slots& s, int k) const {
     std::vector<int> out;
-    for (int32_t i = s.id[k]; i >= 0; i = arena[i].second) out.push_back(arena[i].first);
+    out.push_back(s.label[k]);
+    for (int32_t i = s.prev[k]; i >= 0; i = arena[i].second) out.push_back(arena[i].first);
     std::reverse(out.begin(), out.end());
     return out;
   }
@@ -213,6 +255,7 @@ struct Node {
   T new_t = LogZero<T>(), new_b = LogZero<T>(), new_l = LogZero<T>();
   T state = T(0);   // beam-scorer state: the cached expansion score
   typename Store::Slots old_c, new_c;
+  bool mark = false;  // reclamation: ancestor-or-self of a branch
   Node(Node* p, int l) : parent(p), label(l) {}
   bool active() const { return new_t != LogZero<T>(); }
   bool fresh() const { return old_t == LogZero<T>(); }
@@ -234,12 +277,14 @@ class Decoder {
   // tab: bigram scorer table [C + 1][C] (row from_label + 1), or null for
   // BaseBeamScorer (the identity the reference op uses, kernels.cc:260)
   Decoder(int C, int blank_index, int W, int blank_label, const T* tab = nullptr)
-      : C_(C), blank_(blank_index), W_(W), blank_label_(blank_label), leaves_(W), tab_(tab) { reset(); }
+      : C_(C), blank_(blank_index), W_(W), blank_label_(blank_label), leaves_(W), tab_(tab),
+        scratch_(nullptr, -1) { reset(); }
 
   void reset() {
     leaves_.reset();
     pool_.clear();
     store_.reset_all();
+    gc_next_ = gc_threshold;
     pool_.emplace_back(new N(nullptr, -1));
     root_ = pool_.back().get();
     root_->new_t = T(0);
@@ -259,14 +304,16 @@ class Decoder {
 
     std::vector<N*> branches = leaves_.extract();
     leaves_.reset();
-    {
+    if (count_dups) {
       // frames that start with one entry twice in the beam (reachable with -inf
       // logits: decoder.h:142 pushes every branch, :189-199 re-pushes a branch
-      // that is not Active); reported so the tests can count them
+      // that is not Active); counted only when the tests ask, so the timed
+      // faithful mode does no work the reference does not
       std::vector<N*> sb(branches);
       std::sort(sb.begin(), sb.end());
       if (std::adjacent_find(sb.begin(), sb.end()) != sb.end()) ++dup_frames;
     }
+    if (Store::kLazyNodes && (int64_t)pool_.size() > gc_next_) reclaim(branches);
     if (getenv("ORACLE_TRACE")) {   // debugging aid: frame-start beam, extract order
       printf("frame\n");
       for (N* b : branches) {
@@ -280,8 +327,7 @@ class Decoder {
     }
     for (N* b : branches) {
       b->old_t = b->new_t; b->old_b = b->new_b; b->old_l = b->new_l;
-      b->old_c = b->new_c;
-      Store::clear(b->new_c);
+      store_.roll(b->old_c, b->new_c);
     }
 
     const T pblank = x[blank_] - norm;
@@ -312,7 +358,7 @@ class Decoder {
       if (!admissible(b->old_t)) continue;
       for (int l = 0; l < C_; ++l) {
         if (l == blank_) continue;
-        N* c = child(b, l);
+        N* c = Store::kLazyNodes ? find_child(b, l) : child(b, l);
         if (c->active()) continue;
         const T p = x[l] - norm;
         c->new_b = LogZero<T>();
@@ -327,6 +373,7 @@ class Decoder {
         }
         c->new_t = c->new_l;
         if (admissible(c->new_t)) {
+          if (c == &scratch_) c = adopt(b, l);
           if (leaves_.size() == (size_t)W_) {
             N* bottom = leaves_.peek_bottom();
             bottom->reset_new();
@@ -334,6 +381,8 @@ class Decoder {
           }
           leaves_.push(c);
         } else {
+          // deactivation (decoder.h:200-205); for the scratch node this
+          // leaves it in the never-created state, as required below
           c->reset_old();
           c->reset_new();
           Store::clear(c->old_c);
@@ -386,6 +435,76 @@ class Decoder {
     b->kids.emplace(l, pool_.back().get());
     return pool_.back().get();
   }
+
+  // ---- cost-only node economy of the shared mode ------------------------
+  // A node in the never-created state ("pristine": every probability -inf,
+  // no candidate, no kids) is indistinguishable from one GetChild
+  // (ctc_beam_entry.h:114-122) would build now:
+  //   * new_t/new_b/new_l, new_c and old_c are pristine by definition;
+  //   * old_t/old_b/old_l are pristine too (fresh() reads old_t);
+  //   * `state` is written by ExpandState before every read (decoder.h:171-182
+  //     writes it for an offered child; it is read only for that child and
+  //     for branches, which are never reclaimed);
+  //   * nothing compares node identity except TopN membership, and a reclaimed
+  //     node is in no TopN (reclaim runs between Extract and the first push).
+  // So (1) a child that does not exist yet is evaluated on one scratch node
+  // and only materialised if the TopN accepts it (a rejected one is
+  // deactivated, decoder.h:200-205, i.e. pristine again, exactly as if it had
+  // been created), and (2) pristine nodes that are neither branches nor
+  // ancestors of one are freed.  Results are unchanged; memory drops from
+  // O(W*C*T) nodes to O(live prefixes).
+  N* find_child(N* b, int l) {
+    auto it = b->kids.find(l);
+    if (it != b->kids.end()) return it->second;
+    scratch_.parent = b;
+    scratch_.label = l;
+    return &scratch_;   // pristine (reset after every rejected offer)
+  }
+  N* adopt(N* b, int l) {
+    N* n = new N(b, l);
+    n->old_t = scratch_.old_t; n->old_b = scratch_.old_b; n->old_l = scratch_.old_l;
+    n->new_t = scratch_.new_t; n->new_b = scratch_.new_b; n->new_l = scratch_.new_l;
+    n->state = scratch_.state;
+    n->old_c = scratch_.old_c;
+    n->new_c = scratch_.new_c;
+    pool_.emplace_back(n);
+    b->kids.emplace(l, n);
+    // scratch back to the never-created state
+    scratch_.reset_old();
+    scratch_.reset_new();
+    Store::clear(scratch_.old_c);
+    Store::clear(scratch_.new_c);
+    return n;
+  }
+  static bool pristine(const N* n) {
+    return n->kids.empty() && n->old_t == LogZero<T>() && n->old_b == LogZero<T>() &&
+           n->old_l == LogZero<T>() && n->new_t == LogZero<T>() && n->new_b == LogZero<T>() &&
+           n->new_l == LogZero<T>() && !Store::has(n->old_c, 0) && !Store::has(n->old_c, 1) &&
+           !Store::has(n->new_c, 0) && !Store::has(n->new_c, 1);
+  }
+  void reclaim(const std::vector<N*>& branches) {
+    for (N* b : branches)
+      for (N* a = b; a != nullptr && !a->mark; a = a->parent) a->mark = true;
+    // children are always created after their parent, so a reverse sweep
+    // frees a node's reclaimable kids before the node itself is tested
+    size_t live = 0;
+    for (size_t i = pool_.size(); i-- > 1;) {
+      N* n = pool_[i].get();
+      if (!n->mark && pristine(n)) {
+        n->parent->kids.erase(n->label);
+        pool_[i].reset();
+      }
+    }
+    for (size_t i = 0; i < pool_.size(); ++i) {
+      if (!pool_[i]) continue;
+      pool_[i]->mark = false;
+      if (i != live) pool_[live] = std::move(pool_[i]);
+      ++live;
+    }
+    pool_.resize(live);
+    ++reclaims;
+    gc_next_ = gc_threshold == 1 ? 1 : std::max<int64_t>(gc_threshold, 2 * (int64_t)live);
+  }
   // ctc_beam_entry.h:190-228: receiver r gets a candidate built on
   // src's previous-step candidate of kind from_k (0 = blank-ending).
   void cand(N* r, int to_k, const N* src, int from_k, T p, int label) {
@@ -409,11 +528,16 @@ class Decoder {
 
  public:
   int64_t dup_frames = 0;
+  bool count_dups = false;
+  int64_t gc_threshold = 1 << 20;   // nodes; tests force tiny values
+  int64_t reclaims = 0;
 
  private:
   std::vector<std::unique_ptr<N>> pool_;
   N* root_ = nullptr;
   Store store_;
+  N scratch_;
+  int64_t gc_next_ = 1 << 20;
 };
 
 }  // namespace oracle
@@ -432,17 +556,24 @@ struct OracleResult {
   int32_t* dec_vals;       // concatenation over (b, p) in b-major order
   int32_t* ali_vals;
   double* log_prob;        // [B*P]
-  int64_t dup_frames;      // frames whose beam held one entry twice
+  int64_t dup_frames;      // frames whose beam held one entry twice (flag 1)
+  int64_t reclaims;        // shared-mode node reclamation passes
 };
+
+enum { kFlagCountDups = 1 };
 
 template <class T, class Store>
 static OracleResult* run(const T* x, const int32_t* seq_len, int64_t Tmax, int64_t B, int64_t C,
-                         int W, int P, int merge, int blank_index, int blank_label, const T* tab) {
+                         int W, int P, int merge, int blank_index, int blank_label, const T* tab,
+                         int flags, int64_t gc_threshold) {
   OracleResult* r = new OracleResult();
   memset(r, 0, sizeof(*r));
   std::vector<std::vector<int>> dec_all, ali_all;
   std::vector<double> lp(B * P, 0.0);
   oracle::Decoder<T, Store> dec((int)C, blank_index, W, blank_label, tab);
+  dec.count_dups = (flags & kFlagCountDups) != 0;
+  if (gc_threshold > 0) dec.gc_threshold = gc_threshold;
+  dec.reset();
   std::vector<T> row(C);
   for (int64_t b = 0; b < B; ++b) {
     for (int64_t t = 0; t < seq_len[b]; ++t) {
@@ -453,6 +584,7 @@ static OracleResult* run(const T* x, const int32_t* seq_len, int64_t Tmax, int64
     std::vector<T> lps;
     int st = dec.top_paths(P, merge != 0, paths, aligns, lps, r->no_label_events);
     r->dup_frames = dec.dup_frames;
+    r->reclaims = dec.reclaims;
     if (st != 0) { r->status = st; return r; }
     dec.reset();
     for (int p = 0; p < P; ++p) {
@@ -484,20 +616,29 @@ static OracleResult* run(const T* x, const int32_t* seq_len, int64_t Tmax, int64
 extern "C" {
 
 // dtype 0 = float32, 1 = float64; mode 0 = faithful store, 1 = shared store;
-// table: bigram beam-scorer table [C + 1][C] of dtype, or null (BaseBeamScorer).
-OracleResult* oracle_decode_scored(int dtype, int mode, const void* x, const int32_t* seq_len,
-                                   int64_t T, int64_t B, int64_t C, int W, int P, int merge,
-                                   int blank_index, int blank_label, const void* table) {
+// table: bigram beam-scorer table [C + 1][C] of dtype, or null (BaseBeamScorer);
+// flags: kFlagCountDups; gc_threshold: shared-mode node count that triggers
+// reclamation (<= 0: default 2^20; tests pass 1 to reclaim every frame).
+OracleResult* oracle_decode_ex(int dtype, int mode, const void* x, const int32_t* seq_len,
+                               int64_t T, int64_t B, int64_t C, int W, int P, int merge,
+                               int blank_index, int blank_label, const void* table, int flags,
+                               int64_t gc_threshold) {
   if (dtype == 0) {
     const float* xf = (const float*)x;
     const float* tf = (const float*)table;
-    return mode == 0 ? run<float, oracle::FaithfulStore<float>>(xf, seq_len, T, B, C, W, P, merge, blank_index, blank_label, tf)
-                     : run<float, oracle::SharedStore<float>>(xf, seq_len, T, B, C, W, P, merge, blank_index, blank_label, tf);
+    return mode == 0 ? run<float, oracle::FaithfulStore<float>>(xf, seq_len, T, B, C, W, P, merge, blank_index, blank_label, tf, flags, gc_threshold)
+                     : run<float, oracle::SharedStore<float>>(xf, seq_len, T, B, C, W, P, merge, blank_index, blank_label, tf, flags, gc_threshold);
   }
   const double* xd = (const double*)x;
   const double* td = (const double*)table;
-  return mode == 0 ? run<double, oracle::FaithfulStore<double>>(xd, seq_len, T, B, C, W, P, merge, blank_index, blank_label, td)
-                   : run<double, oracle::SharedStore<double>>(xd, seq_len, T, B, C, W, P, merge, blank_index, blank_label, td);
+  return mode == 0 ? run<double, oracle::FaithfulStore<double>>(xd, seq_len, T, B, C, W, P, merge, blank_index, blank_label, td, flags, gc_threshold)
+                   : run<double, oracle::SharedStore<double>>(xd, seq_len, T, B, C, W, P, merge, blank_index, blank_label, td, flags, gc_threshold);
+}
+
+OracleResult* oracle_decode_scored(int dtype, int mode, const void* x, const int32_t* seq_len,
+                                   int64_t T, int64_t B, int64_t C, int W, int P, int merge,
+                                   int blank_index, int blank_label, const void* table) {
+  return oracle_decode_ex(dtype, mode, x, seq_len, T, B, C, W, P, merge, blank_index, blank_label, table, 0, 0);
 }
 
 OracleResult* oracle_decode(int dtype, int mode, const void* x, const int32_t* seq_len,

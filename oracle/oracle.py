@@ -38,7 +38,8 @@ class _Result(ctypes.Structure):
                 ("dec_vals", ctypes.POINTER(ctypes.c_int32)),
                 ("ali_vals", ctypes.POINTER(ctypes.c_int32)),
                 ("log_prob", ctypes.POINTER(ctypes.c_double)),
-                ("dup_frames", ctypes.c_int64)]
+                ("dup_frames", ctypes.c_int64),
+                ("reclaims", ctypes.c_int64)]
 
 
 _lib = None
@@ -61,19 +62,24 @@ def _load():
             ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         lib.oracle_decode_scored.restype = ctypes.POINTER(_Result)
         lib.oracle_decode_scored.argtypes = lib.oracle_decode.argtypes + [ctypes.c_void_p]
+        lib.oracle_decode_ex.restype = ctypes.POINTER(_Result)
+        lib.oracle_decode_ex.argtypes = lib.oracle_decode_scored.argtypes + [ctypes.c_int, ctypes.c_int64]
         lib.oracle_free.argtypes = [ctypes.POINTER(_Result)]
         _lib = lib
     return _lib
 
 
 def raw_decode(inputs, sequence_length, beam_width, top_paths, merge_repeated=False,
-               blank_index=0, blank_label=-1, mode="shared", stats=None, scorer_table=None):
+               blank_index=0, blank_label=-1, mode="shared", stats=None, scorer_table=None,
+               gc_threshold=0):
     """Returns (dec, ali, log_prob, no_label_events) with dec[b][p] / ali[b][p]
     python lists of ints and log_prob float64 [B, P].  ``stats`` (a dict), if
     given, receives ``duplicate_frames``: frames that started with one entry
-    twice in the beam.  ``scorer_table`` ([C + 1, C], the inputs' dtype): the
-    bigram beam scorer (see ctc_oracle.cpp); None is the reference op's
-    BaseBeamScorer."""
+    twice in the beam, and ``reclaims``: shared-mode node reclamation passes.
+    ``scorer_table`` ([C + 1, C], the inputs' dtype): the bigram beam scorer
+    (see ctc_oracle.cpp); None is the reference op's BaseBeamScorer.
+    ``gc_threshold``: shared-mode node count that triggers reclamation (0: the
+    library default; 1 reclaims every frame, for the tests)."""
     x = np.ascontiguousarray(inputs)
     if x.dtype not in (np.float32, np.float64):
         raise TypeError("inputs must be float32 or float64")
@@ -99,14 +105,16 @@ def raw_decode(inputs, sequence_length, beam_width, top_paths, merge_repeated=Fa
         tab = np.ascontiguousarray(np.asarray(scorer_table, dtype=x.dtype))
         if tab.shape != (C + 1, C):
             raise ValueError("scorer_table must be [num_classes + 1, num_classes]")
-    r = lib.oracle_decode_scored(0 if x.dtype == np.float32 else 1, 0 if mode == "faithful" else 1,
-                                 x.ctypes.data, sl.ctypes.data, T, B, C, int(beam_width),
-                                 int(top_paths), int(bool(merge_repeated)), int(blank_index),
-                                 int(blank_label), None if tab is None else tab.ctypes.data)
+    r = lib.oracle_decode_ex(0 if x.dtype == np.float32 else 1, 0 if mode == "faithful" else 1,
+                             x.ctypes.data, sl.ctypes.data, T, B, C, int(beam_width),
+                             int(top_paths), int(bool(merge_repeated)), int(blank_index),
+                             int(blank_label), None if tab is None else tab.ctypes.data,
+                             1 if stats is not None else 0, int(gc_threshold))
     try:
         res = r.contents
         if stats is not None:
             stats["duplicate_frames"] = int(res.dup_frames)
+            stats["reclaims"] = int(res.reclaims)
         if res.status == 1:
             raise OracleError("requested more paths than the beam width.")
         if res.status == 2:
@@ -156,9 +164,11 @@ def pack_sparse(seqs, B, P):
 
 
 def decode(inputs, sequence_length, beam_width, top_paths, merge_repeated=False,
-           blank_index=0, blank_label=-1, mode="shared", stats=None, scorer_table=None):
+           blank_index=0, blank_label=-1, mode="shared", stats=None, scorer_table=None,
+           gc_threshold=0):
     dec, ali, lp, _ = raw_decode(inputs, sequence_length, beam_width, top_paths,
-                                 merge_repeated, blank_index, blank_label, mode, stats, scorer_table)
+                                 merge_repeated, blank_index, blank_label, mode, stats, scorer_table,
+                                 gc_threshold)
     B = np.asarray(inputs).shape[1]
     di, dv, ds = pack_sparse(dec, B, top_paths)
     ai, av, ash = pack_sparse(ali, B, top_paths)

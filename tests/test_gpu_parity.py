@@ -421,6 +421,37 @@ def test_large_vocab_golden(name):
     np.testing.assert_array_equal(to_numpy(out.log_probability), lp)
 
 
+# ---- full item lengths (BASELINE.json cfg4 T=2000, cfg5 T=3000, cfg3 under the
+# peaky distribution B), against committed oracle outputs
+# (tests/golden/make_fixtures_full.py): the large-C gather, the row's top set,
+# the branch runs and the beam-256 loops over the whole length, where exact
+# float ties between beams are the norm
+
+FULL_PATH = os.path.join(os.path.dirname(__file__), "golden", "full_length.json")
+FULL = json.load(open(FULL_PATH)) if os.path.exists(FULL_PATH) else {}
+
+
+@pytest.mark.parametrize("name", sorted(FULL))
+def test_full_length_golden(name):
+    import hashlib
+    import sys
+    import torch
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import make_fixtures_full
+    fx = FULL[name]
+    case = fx["case"]
+    x, sl = make_fixtures_full.inputs(case)
+    assert hashlib.sha256(x.tobytes()).hexdigest() == fx["sha256"], "input stream changed"
+    _, _, T, B, C, W, P, merge, blank, blabel, _ = case
+    out = ctcext_amd.ctc_ext_beam_search_decoder(
+        torch.as_tensor(x, device="cuda"), torch.as_tensor(sl, device="cuda"),
+        W, P, merge_repeated=merge, blank_index=blank, blank_label=blabel)
+    di, dv, ds = oracle.pack_sparse(fx["decoded"], B, P)
+    ai, av, ash = oracle.pack_sparse(fx["alignment"], B, P)
+    lp = np.asarray([[float.fromhex(h) for h in row] for row in fx["log_probability_hex"]], np.float32)
+    compare(out, oracle.OracleOutput(di, dv, ds, ai, av, ash, lp), P)
+
+
 # ---- beam-scorer hook (util/ctc_beam_scorer.h:31-65).  Parity unpinned: the
 # reference op always runs BaseBeamScorer (kernels.cc:260), so the bigram
 # scorer's only checker is the oracle's restatement of the hook call sites

@@ -57,6 +57,65 @@ def test_oracle_modes_agree_random():
         np.testing.assert_array_equal(a[2], b[2])
 
 
+@pytest.mark.parametrize("family", ["plain", "ties", "neg_inf", "scorer", "large_c"])
+def test_oracle_shared_reclaim_matches_faithful(family):
+    """The shared mode's node economy (lazy child materialisation + reclamation
+    of pristine unreachable nodes, ctc_oracle.cpp Decoder::reclaim) is cost
+    only: with reclamation forced every frame it must equal the faithful
+    (reference-shaped) mode exactly, including the -inf duplicate-entry state
+    and the scorer hook."""
+    from parity_util import random_case
+    rng = np.random.default_rng({"plain": 11, "ties": 12, "neg_inf": 13, "scorer": 14, "large_c": 15}[family])
+    n = 12 if family == "large_c" else 40
+    for _ in range(n):
+        if family == "large_c":
+            x, sl, W, P, kw = random_case(rng, T_max=25, B_max=2, C_min=65, C_max=300, W_max=40)
+        else:
+            x, sl, W, P, kw = random_case(rng, T_max=40, ties=family == "ties", neg_inf=family == "neg_inf")
+        tab = None
+        if family == "scorer":
+            tab = (-np.abs(rng.standard_normal((x.shape[2] + 1, x.shape[2]))) * 2).astype(x.dtype)
+        res = []
+        for mode, gc in (("faithful", 0), ("shared", 1), ("shared", 0)):
+            st = {}
+            try:
+                r = oracle.raw_decode(x, sl, W, P, mode=mode, stats=st, scorer_table=tab, gc_threshold=gc, **kw)
+                res.append((r[0], r[1], r[2].tobytes(), r[3], st["duplicate_frames"]))
+            except oracle.OracleError as e:
+                res.append(str(e))
+        assert res[0] == res[1] == res[2]
+
+
+def test_oracle_shared_reclaim_duplicate_state():
+    """-inf-heavy single items that reach the duplicate-entry state (one
+    BeamEntry twice in the beam, decoder.h:142 + :189-199): the reclaiming
+    shared mode must agree with the faithful mode on those too."""
+    rng = np.random.default_rng(31337)
+    hits = 0
+    for _ in range(3000):
+        T = int(rng.integers(2, 30)); C = int(rng.integers(2, 8)); W = int(rng.integers(1, 10))
+        x = rng.standard_normal((T, 1, C)).astype(np.float32)
+        x[rng.random(x.shape) < (0.3 if rng.random() < 0.5 else 0.5)] = -np.inf
+        P = int(rng.integers(1, W + 1))
+        kw = dict(merge_repeated=bool(rng.integers(2)), blank_index=int(rng.integers(C)),
+                  blank_label=int(rng.integers(-1, C)))
+        st = {}
+        try:
+            a = oracle.raw_decode(x, [T], W, P, mode="faithful", stats=st, **kw)
+        except oracle.OracleError:
+            continue
+        if not st["duplicate_frames"]:
+            continue
+        st2 = {}
+        b = oracle.raw_decode(x, [T], W, P, mode="shared", stats=st2, gc_threshold=1, **kw)
+        assert a[0] == b[0] and a[1] == b[1] and a[2].tobytes() == b[2].tobytes()
+        assert st2["duplicate_frames"] == st["duplicate_frames"]
+        hits += 1
+        if hits == 30:
+            break
+    assert hits == 30
+
+
 def test_oracle_errors():
     x = np.zeros((4, 1, 3), np.float32)
     with pytest.raises(oracle.OracleError, match="requested more paths than the beam width."):
