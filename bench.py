@@ -39,6 +39,14 @@ CONFIGS = {
     "cfg5": (512, 3000, 5000, 256, 1, False, 0),
 }
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# Calibration of the CPU baseline (BASELINE.md "Calibration"): the oracle's
+# reference-cost mode ("port") timed in the build container on SURVEY.md 6's
+# cfg3-shape item (C=29, W=128, P=3, T=1500, merge) ran 81-104 frames/s per
+# core (median of 5 runs ~88) against the compiled reference's 189 frames/s
+# per core measured by the survey on the same container type.  The port is
+# therefore ~0.47x the reference's speed; the reference-equivalent CPU figure
+# is the port's divided by this ratio.
+PORT_OVER_REFERENCE = 0.47
 
 
 HOST_GEN_LIMIT = 4 << 30   # logits above 4 GiB (cfg5: 30.7 GB) are drawn on the device
@@ -123,7 +131,80 @@ def cpu_baseline(cfg, n_workers, t_cap):
             "sample": "%d items x T=%d of the workload shape (C=%d, beam_width=%d, top_paths=%d, "
                       "merge_repeated=%s), oracle reference-cost mode, one item per process"
                       % (n_workers, T, C, W, P, merge),
-            "per_core_value": T / float(np.mean(per_item)), "wall_s": wall}
+            "per_core_value": T / float(np.mean(per_item)), "wall_s": wall,
+            "calibration": {"port_over_reference": PORT_OVER_REFERENCE,
+                            "reference_equivalent_value": frames / wall / PORT_OVER_REFERENCE,
+                            "source": "BASELINE.md Calibration: port vs the survey's compiled reference, "
+                                      "same container type, cfg3-shape item"}}
+
+
+def strong_scaling(args, cfg, world, rank, dev, dec, gather_to_root):
+    """The metric's literal case, a FIXED global batch (BASELINE.json: B=256 on
+    1/2/4/8 GPUs; kernels.cc:68-90 loops over it on one core).
+    N>1: measured -- the global batch (seed 20251015) is split into contiguous
+    shards of B/N items, each rank decodes its shard, the components are
+    gathered to rank 0; barrier + max over ranks as for `value`.
+    N=1: projected -- the same decode call on the first B/N items for N=2,4,8
+    (the shard one GPU of an N-GPU job holds), with device outputs; the N-GPU
+    rate is B*T / that time (the gather's few MB over xGMI are left out)."""
+    import torch
+    import torch.distributed as dist
+    import ctcext_amd
+    from ctcext_amd import _lib
+    B, T, C, W, P, merge, blank = cfg
+    rng = np.random.default_rng(20251015)
+    xg = rng.standard_normal((T, B, C), dtype=np.float32)
+    def run(xs, nb, outputs, gather):
+        slt = torch.full((nb,), T, dtype=torch.int32, device=dev)
+        out = ctcext_amd.ctc_ext_beam_search_decoder(xs, slt, W, P, merge_repeated=merge, blank_index=blank,
+                                                     blank_label=-1, outputs=outputs,
+                                                     flags=_lib.CTCEXT_FLAG_PROFILE)
+        if gather:
+            got = gather_to_root(out, rank * nb, P)
+            if got is not None:
+                [[t.cpu() for t in f] if isinstance(f, list) else f.cpu() for f in got]
+        return out
+    steps = max(2, min(args.steps, 5))
+    if world > 1:
+        nb = B // world
+        xs = torch.as_tensor(np.ascontiguousarray(xg[:, rank * nb:(rank + 1) * nb]), device=dev)
+        run(xs, nb, "device", True)
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            run(xs, nb, "device", True)
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        el = float(el.item())
+        return {"global_batch": B, "batch_per_gpu": nb, "n_gpus": world, "steps": steps,
+                "frames_per_s": B * T * steps / el, "ms_per_step": 1e3 * el / steps,
+                "what": "measured: fixed global batch split over the ranks, RCCL gather to rank 0"}
+    proj = []
+    for n in (1, 2, 4, 8):
+        nb = B // n
+        if nb == 0:
+            continue
+        xs = torch.as_tensor(np.ascontiguousarray(xg[:, :nb]), device=dev)
+        run(xs, nb, "device", False)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        kms = []
+        for _ in range(steps):
+            run(xs, nb, "device", False)
+            kms.append(dec.last_stats["decode_kernel_ms"])
+        torch.cuda.synchronize()
+        ms = 1e3 * (time.perf_counter() - t0) / steps
+        proj.append({"n_gpus": n, "batch_per_gpu": nb, "ms_per_step": ms, "decode_kernel_ms": float(np.mean(kms)),
+                     "projected_frames_per_s": B * T / (ms * 1e-3)})
+    for p in proj:
+        p["efficiency_vs_linear"] = p["projected_frames_per_s"] / (proj[0]["projected_frames_per_s"] * p["n_gpus"])
+    return {"global_batch": B, "what": "projected from one GPU: per-GPU time of the B/N-item shard "
+                                      "(device outputs, gather excluded)", "curve": proj}
 
 
 def main():
@@ -141,6 +222,10 @@ def main():
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-host-io", action="store_true", help="skip the host-I/O (PCIe-inclusive) extra")
     ap.add_argument("--seq-len", type=int, default=0, help="diagnostics: override T (not a bench line)")
+    ap.add_argument("--batch-per-gpu", type=int, default=0, help="diagnostics: override B per GPU (not a bench line)")
+    ap.add_argument("--no-strong", action="store_true",
+                    help="skip the strong-scaling extra (N=1: the per-GPU latency at the B=256/N shards; "
+                         "N>1: the measured global-B=256 split)")
     args = ap.parse_args()
 
     import torch
@@ -170,6 +255,8 @@ def main():
     cfg = CONFIGS[args.config]
     if args.seq_len:
         cfg = (cfg[0], args.seq_len) + cfg[2:]
+    if args.batch_per_gpu:
+        cfg = (args.batch_per_gpu,) + cfg[1:]
     B, T, C, W, P, merge, blank = cfg
     x_np, x, sl_np, gen = make_inputs(cfg, rank, dev)
     sl = torch.as_tensor(sl_np, device=dev)
@@ -231,7 +318,7 @@ def main():
             traffic_src = "stale: %s is of build %s, this is %s" % (os.path.relpath(pmc, ROOT),
                                                                    pj.get("lib_sha16"), lib_hash())
     metric = "decoded frames/sec at B=256, T=1500, C=29, beam_width=128; 1/2/4/8 GPUs"   # BASELINE.json
-    if args.config != "cfg3" or args.seq_len:   # diagnostics lines name their own workload
+    if args.config != "cfg3" or args.seq_len or args.batch_per_gpu:   # diagnostics lines name their own workload
         metric = "decoded frames/sec at B=%d, T=%d, C=%d, beam_width=%d (%s, not the BASELINE metric)" % (
             B * world, T, C, W, args.config)
     res = {
@@ -280,6 +367,8 @@ def main():
         io_s = (time.perf_counter() - t1) / n_io
         res["host_io"] = {"frames_per_s": int(sl_np.sum()) / io_s, "ms_per_step": 1e3 * io_s,
                           "steps": n_io, "what": "host numpy logits in, host numpy outputs out (PCIe both ways)"}
+    if not args.no_strong and not args.seq_len and not args.batch_per_gpu and B % 2 == 0:
+        res["strong"] = strong_scaling(args, cfg, world, rank, dev, dec, gather_to_root)
     if rank == 0 and world == 1 and not args.no_cpu:
         share, info = cpu_share()
         nw = args.cpu_workers or share

@@ -432,6 +432,13 @@ static int run_decode(ctcext_decoder* d, const ctcext_decode_args* a, const std:
       x = (const T*)a->inputs;
       xstride = B;
       sl = a->sequence_length;
+    } else if (v.nb == 0) {
+      // an empty root shard (B < n_devices, no frames anywhere): nothing to
+      // copy; enqueue_shard only sizes the root's whole-batch buffers and
+      // launches no kernel over zero items
+      x = nullptr;
+      xstride = 0;
+      sl = nullptr;
     } else {
       const size_t row = (size_t)v.nb * (size_t)C * ts;
       HIP_OR_FAIL(v.x.ensure(row * (size_t)T_ + 16));

@@ -3187,6 +3187,7 @@ __global__ __launch_bounds__(64) void ctcx_row_norm(const T* __restrict__ x, con
   if (valid) norm[row] = m + norm_log(s);
 }
 
+#if CTCX_PART == 0
 // ---------------------------------------------------------------------------
 // Backward walks over the records.  which = 0: decoded labels (LabelSeq,
 // ctc_beam_entry.h:123-136); which = 1: best alignment (AlignmentLabelSeq +
@@ -3283,6 +3284,8 @@ __global__ __launch_bounds__(64) void ctcx_pack(PackParams pp) {
   }
 }
 
+#endif  // CTCX_PART == 0 (the non-template kernels)
+
 }  // namespace ctcx
 
 // ---------------------------------------------------------------------------
@@ -3290,7 +3293,7 @@ __global__ __launch_bounds__(64) void ctcx_pack(PackParams pp) {
 namespace ctcx {
 
 template <typename T, int RN, int WC, bool BIG, class SC>
-static hipError_t launch_decode_c(const DecodeParams<T>& p, hipStream_t s) {
+hipError_t launch_decode_c(const DecodeParams<T>& p, hipStream_t s) {
   const size_t lds = decode_lds_bytes(WC > 0 ? WC : p.W, p.C, (int)sizeof(T), SC::kStateful);
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)ctcx_beam_decode<T, RN, WC, BIG, SC>,
@@ -3301,6 +3304,80 @@ static hipError_t launch_decode_c(const DecodeParams<T>& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+// The decode kernel's instantiations are split over several compilations of
+// this file (CTCX_PART, csrc/Makefile), so the build runs them in parallel:
+// part 0 holds everything else and the dispatcher; parts 1..6 one group of
+// kernel instantiations each.
+#define CTCX_DECODE_INSTANCES(X)                                                              \
+  X(1, float, 1, 128, false, BaseBeamScorer<float>) X(1, float, 1, 0, false, BaseBeamScorer<float>) \
+  X(1, float, 2, 256, false, BaseBeamScorer<float>) X(1, float, 2, 0, false, BaseBeamScorer<float>) \
+  X(1, float, 4, 0, false, BaseBeamScorer<float>)                                             \
+  X(2, float, 1, 128, true, BaseBeamScorer<float>) X(2, float, 1, 0, true, BaseBeamScorer<float>)   \
+  X(3, float, 2, 256, true, BaseBeamScorer<float>) X(3, float, 2, 0, true, BaseBeamScorer<float>)   \
+  X(3, float, 4, 0, true, BaseBeamScorer<float>)                                              \
+  X(4, double, 1, 128, false, BaseBeamScorer<double>) X(4, double, 1, 0, false, BaseBeamScorer<double>) \
+  X(4, double, 2, 256, false, BaseBeamScorer<double>) X(4, double, 2, 0, false, BaseBeamScorer<double>) \
+  X(4, double, 4, 0, false, BaseBeamScorer<double>)                                           \
+  X(5, double, 1, 128, true, BaseBeamScorer<double>) X(5, double, 1, 0, true, BaseBeamScorer<double>) \
+  X(5, double, 2, 256, true, BaseBeamScorer<double>) X(5, double, 2, 0, true, BaseBeamScorer<double>) \
+  X(5, double, 4, 0, true, BaseBeamScorer<double>)                                            \
+  X(6, float, 1, 128, false, BigramBeamScorer<float>) X(6, float, 1, 0, false, BigramBeamScorer<float>) \
+  X(6, float, 2, 256, false, BigramBeamScorer<float>) X(6, float, 2, 0, false, BigramBeamScorer<float>) \
+  X(6, float, 4, 0, false, BigramBeamScorer<float>)                                           \
+  X(6, float, 1, 128, true, BigramBeamScorer<float>) X(6, float, 1, 0, true, BigramBeamScorer<float>) \
+  X(6, float, 2, 256, true, BigramBeamScorer<float>) X(6, float, 2, 0, true, BigramBeamScorer<float>) \
+  X(6, float, 4, 0, true, BigramBeamScorer<float>)                                            \
+  X(7, double, 1, 128, false, BigramBeamScorer<double>) X(7, double, 1, 0, false, BigramBeamScorer<double>) \
+  X(7, double, 2, 256, false, BigramBeamScorer<double>) X(7, double, 2, 0, false, BigramBeamScorer<double>) \
+  X(7, double, 4, 0, false, BigramBeamScorer<double>)                                         \
+  X(7, double, 1, 128, true, BigramBeamScorer<double>) X(7, double, 1, 0, true, BigramBeamScorer<double>) \
+  X(7, double, 2, 256, true, BigramBeamScorer<double>) X(7, double, 2, 0, true, BigramBeamScorer<double>) \
+  X(7, double, 4, 0, true, BigramBeamScorer<double>)
+
+#ifndef CTCX_PART
+#define CTCX_PART 0
+#endif
+#define CTCX_IF_1(...)
+#define CTCX_IF_2(...)
+#define CTCX_IF_3(...)
+#define CTCX_IF_4(...)
+#define CTCX_IF_5(...)
+#define CTCX_IF_6(...)
+#define CTCX_IF_7(...)
+#if CTCX_PART == 1
+#undef CTCX_IF_1
+#define CTCX_IF_1(...) __VA_ARGS__
+#elif CTCX_PART == 2
+#undef CTCX_IF_2
+#define CTCX_IF_2(...) __VA_ARGS__
+#elif CTCX_PART == 3
+#undef CTCX_IF_3
+#define CTCX_IF_3(...) __VA_ARGS__
+#elif CTCX_PART == 4
+#undef CTCX_IF_4
+#define CTCX_IF_4(...) __VA_ARGS__
+#elif CTCX_PART == 5
+#undef CTCX_IF_5
+#define CTCX_IF_5(...) __VA_ARGS__
+#elif CTCX_PART == 6
+#undef CTCX_IF_6
+#define CTCX_IF_6(...) __VA_ARGS__
+#elif CTCX_PART == 7
+#undef CTCX_IF_7
+#define CTCX_IF_7(...) __VA_ARGS__
+#endif
+#define CTCX_IF_PART(P, ...) CTCX_IF_##P(__VA_ARGS__)
+#if CTCX_PART == 0
+#define CTCX_X(P, T, RN, WC, BIG, SC) \
+  extern template hipError_t launch_decode_c<T, RN, WC, BIG, SC>(const DecodeParams<T>&, hipStream_t);
+#else
+#define CTCX_X(P, T, RN, WC, BIG, SC) \
+  CTCX_IF_PART(P, template hipError_t launch_decode_c<T, RN, WC, BIG, SC>(const DecodeParams<T>&, hipStream_t);)
+#endif
+CTCX_DECODE_INSTANCES(CTCX_X)
+#undef CTCX_X
+
+#if CTCX_PART == 0
 // BIG (C > 64): the grow loop's branch/window skipping by row-block maxima is
 // compiled in; small-C builds keep the leaner loop (its register allocation is
 // what cfg3 runs on)
@@ -3314,10 +3391,11 @@ hipError_t launch_decode(const DecodeParams<T>& p, hipStream_t s) {
   if (p.B == 0) return hipSuccess;
   // RN registers per lane hold the min-child of the (W + 1) / 2 internal heap
   // nodes; the compile-time layouts (WC) are used whenever they fit the LDS
-  if (p.scorer_tab) {   // the bigram scorer: runtime LDS layout only
+  if (p.scorer_tab) {   // the bigram scorer: the same compile-time layouts (with its state arrays)
     using SC = BigramBeamScorer<T>;
-    if (p.W <= 128) return launch_decode_r<T, 1, 0, SC>(p, s);
-    if (p.W <= 256) return launch_decode_r<T, 2, 0, SC>(p, s);
+    auto fits_s = [&](int wc) { return decode_lds_bytes(wc, p.C, (int)sizeof(T), true) <= kLdsBytes; };
+    if (p.W <= 128) return fits_s(128) ? launch_decode_r<T, 1, 128, SC>(p, s) : launch_decode_r<T, 1, 0, SC>(p, s);
+    if (p.W <= 256) return fits_s(256) ? launch_decode_r<T, 2, 256, SC>(p, s) : launch_decode_r<T, 2, 0, SC>(p, s);
     return launch_decode_r<T, 4, 0, SC>(p, s);
   }
   auto fits = [&](int wc) { return decode_lds_bytes(wc, p.C, (int)sizeof(T)) <= kLdsBytes; };
@@ -3361,5 +3439,6 @@ hipError_t launch_pack(const PackParams& pp, hipStream_t s) {
   hipLaunchKernelGGL(ctcx_pack, dim3((unsigned)n), dim3(64), 0, s, pp);
   return hipGetLastError();
 }
+#endif  // CTCX_PART == 0
 
 }  // namespace ctcx

@@ -261,6 +261,11 @@ def ctc_ext_beam_search_decoder(inputs, sequence_length, beam_width, top_paths,
         stream = None
     a = _args(x_ptr, shape, code, on_device, sl_ptr, sl_shape, beam_width, top_paths, merge_repeated,
               blank_index, blank_label, flags, stream)
+    # the reference's shape/length checks run behind the C ABI, before any
+    # device work (kernels.cc:97-139)
+    rc = lib.ctcext_validate(ctypes.byref(a))
+    if rc != _lib.CTCEXT_OK:
+        _raise(lib, rc)
     if scorer_table is not None:
         C = int(shape[2]) if len(shape) == 3 else 0
         if on_device:
@@ -276,11 +281,10 @@ def ctc_ext_beam_search_decoder(inputs, sequence_length, beam_width, top_paths,
                              % (C + 1, C, tuple(tab.shape)))
         keep.append(tab)
         a.scorer = _lib.CTCEXT_SCORER_BIGRAM
-    # the reference's shape/length checks run behind the C ABI, before any
-    # device work (kernels.cc:97-139)
-    rc = lib.ctcext_validate(ctypes.byref(a))
-    if rc != _lib.CTCEXT_OK:
-        _raise(lib, rc)
+        # the library checks the table's entries (<= 0) before decoding
+        rc = lib.ctcext_validate(ctypes.byref(a))
+        if rc != _lib.CTCEXT_OK:
+            _raise(lib, rc)
     if devices is not None:
         devs = tuple(int(d) for d in devices)
         if on_device and devs[0] != index:

@@ -84,6 +84,8 @@ def test_sharded_handle_errors_match():
         assert e.value.message == "sequence_length(0) <= 5"
 
 
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs: on one GPU the current "
+                    "device and the library's device coincide, so restoration is not observable")
 def test_current_device_is_restored():
     # the C ABI saves and restores the caller's HIP device (torch reads the
     # same runtime's current device)
@@ -96,6 +98,79 @@ def test_current_device_is_restored():
         ctcext_amd.ctc_ext_beam_search_decoder(x, [10, 10], 4, 1, devices=[0, 0])
         assert torch.cuda.current_device() == cur
     torch.cuda.set_device(0)
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs (the cross-device xGMI path: "
+                    "peer access, strided shard copies out of the root's memory, peer-copy gather)")
+def test_sharded_handle_two_distinct_devices():
+    rng = np.random.default_rng(2)
+    x = rng.standard_normal((80, 9, 29)).astype(np.float32)
+    sl = rng.integers(0, 81, size=9).astype(np.int32)
+    kw = dict(merge_repeated=True, blank_index=0, blank_label=-1)
+    one = ctcext_amd.ctc_ext_beam_search_decoder(x, sl, 32, 2, **kw)
+    for xin, slin in ((x, sl), (torch.as_tensor(x, device="cuda:0"), torch.as_tensor(sl, device="cuda:0"))):
+        many = ctcext_amd.ctc_ext_beam_search_decoder(xin, slin, 32, 2, devices=[0, 1], **kw)
+        _same(many, one, 2)
+
+
+@pytest.mark.parametrize("device_in", [False, True])
+def test_sharded_root_shard_empty(device_in):
+    # B < n_devices with every length <= 0: the split by count gives the root
+    # no items; its input copies are skipped (ctcext_capi.hip run_decode)
+    x = np.random.default_rng(3).standard_normal((4, 1, 6)).astype(np.float32)
+    sl = np.array([0], np.int32)
+    xin = torch.as_tensor(x, device="cuda:0") if device_in else x
+    slin = torch.as_tensor(sl, device="cuda:0") if device_in else sl
+    one = ctcext_amd.ctc_ext_beam_search_decoder(xin, slin, 4, 1)
+    many = ctcext_amd.ctc_ext_beam_search_decoder(xin, slin, 4, 1, devices=[0, 0])
+    _same(many, one, 1)
+    compare(one, oracle.decode(x, sl, 4, 1), 1)
+
+
+def _memory_probe():
+    import psutil
+    free, _ = torch.cuda.mem_get_info(0)
+    hs = torch.cuda.host_memory_stats() if hasattr(torch.cuda, "host_memory_stats") else {}
+    return free, hs.get("reserved_bytes.current", hs.get("allocated_bytes.current", 0)), \
+        psutil.Process().memory_info().rss
+
+
+@pytest.mark.parametrize("devices", [None, [0, 0]])
+def test_no_memory_growth_over_1000_calls(devices):
+    """The reference's memory-leak test (python/ops/..._test.py:102-123: 1000
+    calls, memory must not grow), on what this path allocates: device memory
+    (the library's grow-only workspace, torch's caching allocator for device
+    outputs), the pinned host pool behind host outputs, and this process's
+    RSS.  After the first calls have sized every pool, 1000 more calls must
+    not grow any of them."""
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((60, 6, 29)).astype(np.float32)
+    sl = np.array([60, 41, 60, 7, 1, 60], np.int32)
+    xd, sld = torch.as_tensor(x, device="cuda:0"), torch.as_tensor(sl, device="cuda:0")
+    kw = dict(merge_repeated=True, blank_index=0, blank_label=-1, devices=devices)
+
+    def call(i):
+        if i % 2:
+            out = ctcext_amd.ctc_ext_beam_search_decoder(xd, sld, 16, 2, **kw)
+        else:
+            out = ctcext_amd.ctc_ext_beam_search_decoder(x, sl, 16, 2, **kw)
+        return out
+    first = call(0)
+    for i in range(1, 20):
+        call(i)
+    torch.cuda.synchronize()
+    free0, pinned0, rss0 = _memory_probe()
+    for i in range(1000):
+        out = call(i)
+    torch.cuda.synchronize()
+    free1, pinned1, rss1 = _memory_probe()
+    _same(out, ctcext_amd.ctc_ext_beam_search_decoder(xd, sld, 16, 2, **kw), 2)
+    _same(first, out, 2)
+    assert free1 >= free0, ("device memory shrank", free0, free1)
+    assert pinned1 <= pinned0, ("pinned host pool grew", pinned0, pinned1)
+    # RSS: the Python objects of 1000 calls come and go; a leak of the ~50 KB
+    # of outputs per call would add ~50 MB
+    assert rss1 - rss0 < 8 << 20, ("host RSS grew", rss0, rss1)
 
 
 def test_two_ranks_hip_decoder_gather(tmp_path):
