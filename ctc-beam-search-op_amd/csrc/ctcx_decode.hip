@@ -181,9 +181,9 @@ struct Ctx {
   CTCX_LDS int* alias;
   CTCX_LDS T* row;
   CTCX_LDS int* misc;
-  // prefix identity: 128-bit hash of each branch's label prefix and of its
-  // parent's, [buf][i]; htab maps the hash of a frame's new leaves to position
-  CTCX_LDS uint64_t* ha[2]; CTCX_LDS uint64_t* hb[2]; CTCX_LDS uint64_t* pha[2]; CTCX_LDS uint64_t* phb[2];
+  // prefix identity: 128-bit hash of each branch's label prefix, [buf][i];
+  // htab maps the hash of a frame's new leaves to position
+  CTCX_LDS uint64_t* ha[2]; CTCX_LDS uint64_t* hb[2];
   CTCX_LDS int* htab;
   CTCX_LDS uint64_t* bloom;   // per branch: label bits (l & 63) of children evicted this frame
   CTCX_LDS HE<T>* he;  // TopN elements_, position p at he[p + 1]
@@ -242,22 +242,48 @@ __host__ __device__ __forceinline__ void hmix(uint64_t a, uint64_t b, int l, uin
 }
 constexpr uint64_t kRootHa = 0x243F6A8885A308D3ull, kRootHb = 0x13198A2E03707344ull;
 
+// The parent's prefix hash from a node's own (hmix is invertible: fmix64 and
+// both label steps are bijections), so it need not be stored per branch.
+__host__ __device__ constexpr uint64_t inv_odd64(uint64_t a) {
+  uint64_t x = a;                                    // correct to 3 bits (a odd)
+  for (int i = 0; i < 6; ++i) x *= 2ull - a * x;     // Newton: doubles the bits
+  return x;
+}
+__host__ __device__ __forceinline__ uint64_t fmix64_inv(uint64_t k) {
+  k ^= k >> 33; k *= inv_odd64(0xc4ceb9fe1a85ec53ull);
+  k ^= k >> 33; k *= inv_odd64(0xff51afd7ed558ccdull);
+  k ^= k >> 33;
+  return k;
+}
+__host__ __device__ __forceinline__ void hmix_inv(uint64_t oa, uint64_t ob, int l, uint64_t& a, uint64_t& b) {
+  const uint64_t x = (uint64_t)(uint32_t)l + 1ull;
+  a = fmix64_inv(oa) ^ (x * 0x9E3779B97F4A7C15ull);
+  b = fmix64_inv(ob) - x * 0xD6E8FEB86659FD93ull - 0x632BE59BD9B4E019ull;
+}
+static_assert(inv_odd64(0xff51afd7ed558ccdull) * 0xff51afd7ed558ccdull == 1ull, "inverse");
+static_assert(inv_odd64(0xc4ceb9fe1a85ec53ull) * 0xc4ceb9fe1a85ec53ull == 1ull, "inverse");
+
 // LDS layout for a beam of up to Wcap (the kernel's compile-time capacity, or
 // the runtime W for the WC = 0 instantiations).  Every array sits at an offset
 // that depends on Wcap only -- the C-sized logit row comes last -- so with a
 // compile-time Wcap all of them are instruction immediates instead of ~45
 // pointer SGPRs.  decode_lds_bytes (ctcx_kernels.h) mirrors this sum.
 template <typename T>
-__host__ __device__ void carve(Ctx<T>& cx, CTCX_LDS char* base, int Wcap, int W, int C, bool scored = false) {
+__host__ __device__ __forceinline__ void carve(Ctx<T>& cx, CTCX_LDS char* base, int Wcap, int W, int C, bool scored,
+                                               bool inplace) {
+  // inplace (large C, decode_inplace): one buffer of branch arrays, updated in
+  // place by the commit.  The caller passes a compile-time value, so every
+  // offset stays an immediate.
   const size_t ENC = 3 * (size_t)Wcap + 2;
+  const int nbuf = inplace ? 1 : 2;
   auto a16 = [](size_t v) { return (v + 15) & ~(size_t)15; };
   CTCX_LDS char* p = base;
-  for (int b = 0; b < 2; ++b) {
+  for (int b = 0; b < nbuf; ++b) {
     CTCX_LDS T* q = (CTCX_LDS T*)p;
     cx.ot[b] = q; cx.ob[b] = q + Wcap; cx.ol[b] = q + 2 * Wcap; cx.cb[b] = q + 3 * Wcap; cx.cn[b] = q + 4 * Wcap;
     p += a16(5 * (size_t)Wcap * sizeof(T));
   }
-  for (int b = 0; b < 2; ++b) {
+  for (int b = 0; b < nbuf; ++b) {
     CTCX_LDS int* q = (CTCX_LDS int*)p;
     cx.lab[b] = q; cx.par[b] = q + Wcap; cx.flg[b] = q + 2 * Wcap;
     p += a16(3 * (size_t)Wcap * 4);
@@ -280,17 +306,21 @@ __host__ __device__ void carve(Ctx<T>& cx, CTCX_LDS char* base, int Wcap, int W,
   }
   cx.heap = (CTCX_LDS int*)p; p += a16(((size_t)Wcap + 1) * 4);
   cx.tops = (CTCX_LDS int*)p; p += a16(((size_t)Wcap + 1) * 4);
-  cx.freel = (CTCX_LDS int*)p; p += a16(ENC * 4);
   cx.sorted = (CTCX_LDS int*)p; p += a16((size_t)Wcap * 4);
   cx.alias = (CTCX_LDS int*)p; p += a16((size_t)Wcap * 4);
   cx.misc = (CTCX_LDS int*)p; p += 64;
-  for (int b = 0; b < 2; ++b) {
+  for (int b = 0; b < nbuf; ++b) {
     CTCX_LDS uint64_t* q = (CTCX_LDS uint64_t*)p;
-    cx.ha[b] = q; cx.hb[b] = q + Wcap; cx.pha[b] = q + 2 * Wcap; cx.phb[b] = q + 3 * Wcap;
-    p += 4 * (size_t)Wcap * 8;
+    cx.ha[b] = q; cx.hb[b] = q + Wcap;
+    p += 2 * (size_t)Wcap * 8;
   }
   cx.hts = htab_size(Wcap);
   cx.htab = (CTCX_LDS int*)p;
+  // the free list / slot map (ENC ints, literal_step and the last frame's
+  // TopPaths) shares the room of the hash table and the bloom (>= 16 Wcap
+  // bytes): neither is live while it is (the commit rebuilds the table, the
+  // next frame's roll clears the bloom)
+  cx.freel = (CTCX_LDS int*)p;
   p += a16(4 * (size_t)cx.hts);
   cx.bloom = (CTCX_LDS uint64_t*)p;
   p += a16(8 * (size_t)Wcap);
@@ -302,8 +332,13 @@ __host__ __device__ void carve(Ctx<T>& cx, CTCX_LDS char* base, int Wcap, int W,
   p += ((size_t)cx.hdum + 64) * sizeof(HE<T>);
   cx.est[0] = cx.est[1] = cx.eest = nullptr;
   if (scored) {
-    cx.est[0] = (CTCX_LDS T*)p; cx.est[1] = cx.est[0] + Wcap; cx.eest = cx.est[1] + Wcap;
-    p += a16((2 * (size_t)Wcap + ENC) * sizeof(T));
+    cx.est[0] = (CTCX_LDS T*)p; cx.est[1] = cx.est[0] + (nbuf - 1) * Wcap; cx.eest = cx.est[0] + nbuf * Wcap;
+    p += a16(((size_t)nbuf * Wcap + ENC) * sizeof(T));
+  }
+  if (nbuf == 1) {   // both frame parities name the one buffer
+    cx.ot[1] = cx.ot[0]; cx.ob[1] = cx.ob[0]; cx.ol[1] = cx.ol[0]; cx.cb[1] = cx.cb[0]; cx.cn[1] = cx.cn[0];
+    cx.lab[1] = cx.lab[0]; cx.par[1] = cx.par[0]; cx.flg[1] = cx.flg[0];
+    cx.ha[1] = cx.ha[0]; cx.hb[1] = cx.hb[0];
   }
   cx.row = (CTCX_LDS T*)p;
   cx.wcap = Wcap;
@@ -2912,7 +2947,7 @@ template <typename T, int RN, int WC, bool BIG, class SC>
 __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   Ctx<T> cx;
-  carve(cx, (CTCX_LDS char*)lds, WC > 0 ? WC : prm.W, prm.W, (int)prm.C, SC::kStateful);
+  carve(cx, (CTCX_LDS char*)lds, WC > 0 ? WC : prm.W, prm.W, (int)prm.C, SC::kStateful, BIG);   // BIG == decode_inplace(C)
   cx.blank = prm.blank;
   cx.sctab = prm.scorer_tab;
   const int lane = threadIdx.x;
@@ -2929,7 +2964,7 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     cx.lab[0][0] = -1; cx.par[0][0] = -1; cx.flg[0][0] = F_ROOT;
     cx.ot[0][0] = T(0); cx.ob[0][0] = T(0); cx.ol[0][0] = ninf<T>();
     cx.cb[0][0] = T(0); cx.cn[0][0] = T(0);
-    cx.ha[0][0] = kRootHa; cx.hb[0][0] = kRootHb; cx.pha[0][0] = 0; cx.phb[0][0] = 0;
+    cx.ha[0][0] = kRootHa; cx.hb[0][0] = kRootHb;
     cx.head[0] = -1;
     cx.alias[0] = 0;
     if constexpr (SC::kStateful) cx.est[0][0] = T(0);   // InitializeState (decoder.h:226)
@@ -2996,7 +3031,12 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     if (prof) pc[5] += t3 - t2;
 
     // ---- commit: records + next frame's branch arrays (sorted order) ----
-    const int nx = buf ^ 1;
+    // Large C: the arrays are updated in place, so every read of the
+    // frame-start arrays (by source position) is taken into registers before
+    // the first write (by sorted position); KM positions per lane.
+    constexpr bool INPLACE = BIG;
+    constexpr int KM = (WC > 0 ? WC : 512) / 64;
+    const int nx = INPLACE ? buf : buf ^ 1;
     for (int i = lane; i < nb; i += 64) cx.newpos[i] = -1;
     __syncthreads();
     // (an entry the beam holds twice: its first position is the canonical one,
@@ -3010,63 +3050,97 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     for (int q = lane; q < cx.hts; q += 64) cx.htab[q] = -1;
     __syncthreads();
     // prefix hashes of the new leaves; new children go into the hash table
-    for (int k = lane; k < n; k += 64) {
-      const uint32_t kd = cx.ekind[cx.sorted[k]];
-      const int src = (int)(kd >> 1);
-      uint64_t ha, hb, pa, pb;
-      if (kd & 1u) {
-        pa = sel(cx.ha, buf)[src]; pb = sel(cx.hb, buf)[src];
-        hmix(pa, pb, cx.elab[cx.sorted[k]], ha, hb);
-        int q = (int)(ha & (uint64_t)(cx.hts - 1));
-        int expect = -1;
-        while ((!dup_next || cx.alias[k] == k) &&
-               !__hip_atomic_compare_exchange_strong(&cx.htab[q], &expect, k, __ATOMIC_RELAXED,
-                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-          q = (q + 1) & (cx.hts - 1);
-          expect = -1;
+    {
+      uint64_t nha[KM], nhb[KM];
+#pragma unroll
+      for (int j = 0; j < KM; ++j) {
+        const int k = lane + 64 * j;
+        nha[j] = nhb[j] = 0;
+        if (k < n) {
+          const int e = cx.sorted[k];
+          const uint32_t kd = cx.ekind[e];
+          const int src = (int)(kd >> 1);
+          nha[j] = sel(cx.ha, buf)[src];
+          nhb[j] = sel(cx.hb, buf)[src];
+          if (kd & 1u) hmix(nha[j], nhb[j], cx.elab[e], nha[j], nhb[j]);
         }
-      } else {
-        ha = sel(cx.ha, buf)[src]; hb = sel(cx.hb, buf)[src];
-        pa = sel(cx.pha, buf)[src]; pb = sel(cx.phb, buf)[src];
       }
-      sel(cx.ha, nx)[k] = ha; sel(cx.hb, nx)[k] = hb; sel(cx.pha, nx)[k] = pa; sel(cx.phb, nx)[k] = pb;
-    }
-    __syncthreads();
-    Rec* rout = prm.rec + ((int64_t)b * prm.Tmax + t) * W;
-    for (int k = lane; k < n; k += 64) {
-      const int e = cx.sorted[k];
-      const uint32_t kd = cx.ekind[e];
-      const int src = (int)(kd >> 1);
-      const bool isnew = (kd & 1u) != 0;
-      const int pf = sel(cx.flg, buf)[src];
-      int parent, fl;
-      if (isnew) {
-        parent = cx.newpos[src];
-        fl = (pf & F_ROOT) ? F_PROOT : 0;
-      } else {
-        const int pp = sel(cx.par, buf)[src];
-        parent = pp >= 0 ? cx.newpos[pp] : -1;
-        fl = pf & (F_ROOT | F_PROOT);
-        if (pp < 0 && !(pf & F_ROOT)) {
-          // the parent node was not in the beam; it may have re-entered this
-          // frame as a new child (the reference finds it through the trie)
-          const uint64_t pa = sel(cx.pha, nx)[k], pb = sel(cx.phb, nx)[k];
-          for (int q = (int)(pa & (uint64_t)(cx.hts - 1));; q = (q + 1) & (cx.hts - 1)) {
-            const int c = cx.htab[q];
-            if (c < 0) break;
-            if (sel(cx.ha, nx)[c] == pa && sel(cx.hb, nx)[c] == pb) { parent = c; break; }
+      if constexpr (INPLACE) __syncthreads();
+#pragma unroll
+      for (int j = 0; j < KM; ++j) {
+        const int k = lane + 64 * j;
+        if (k < n) {
+          sel(cx.ha, nx)[k] = nha[j];
+          sel(cx.hb, nx)[k] = nhb[j];
+          if ((cx.ekind[cx.sorted[k]] & 1u) && (!dup_next || cx.alias[k] == k)) {
+            int q = (int)(nha[j] & (uint64_t)(cx.hts - 1));
+            int expect = -1;
+            while (!__hip_atomic_compare_exchange_strong(&cx.htab[q], &expect, k, __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+              q = (q + 1) & (cx.hts - 1);
+              expect = -1;
+            }
           }
         }
       }
-      const int ef = cx.eflg[e];
-      fl |= ef & (F_HB | F_HN);
-      sel(cx.lab, nx)[k] = cx.elab[e];
-      sel(cx.par, nx)[k] = parent;
-      sel(cx.flg, nx)[k] = fl;
-      sel(cx.ot, nx)[k] = cx.et[e]; sel(cx.ob, nx)[k] = cx.eb[e]; sel(cx.ol, nx)[k] = cx.el[e];
-      sel(cx.cb, nx)[k] = cx.ecb[e]; sel(cx.cn, nx)[k] = cx.ecn[e];
-      if constexpr (SC::kStateful) sel(cx.est, nx)[k] = cx.eest[e];
-      rout[k] = rec_pack(kd, cx.elab[e], (ef & F_HB) ? cx.ebpb[e] : kBpNone, (ef & F_HN) ? cx.ebpn[e] : kBpNone);
+    }
+    __syncthreads();
+    Rec* rout = prm.rec + ((int64_t)b * prm.Tmax + t) * W;
+    {
+      int npar[KM], nfl[KM];
+#pragma unroll
+      for (int j = 0; j < KM; ++j) {
+        const int k = lane + 64 * j;
+        npar[j] = -1;
+        nfl[j] = 0;
+        if (k < n) {
+          const int e = cx.sorted[k];
+          const uint32_t kd = cx.ekind[e];
+          const int src = (int)(kd >> 1);
+          const bool isnew = (kd & 1u) != 0;
+          const int pf = sel(cx.flg, buf)[src];
+          int parent, fl;
+          if (isnew) {
+            parent = cx.newpos[src];
+            fl = (pf & F_ROOT) ? F_PROOT : 0;
+          } else {
+            const int pp = sel(cx.par, buf)[src];
+            parent = pp >= 0 ? cx.newpos[pp] : -1;
+            fl = pf & (F_ROOT | F_PROOT);
+            if (pp < 0 && !(pf & F_ROOT)) {
+              // the parent node was not in the beam; it may have re-entered this
+              // frame as a new child (the reference finds it through the trie)
+              uint64_t pa, pb;
+              hmix_inv(sel(cx.ha, nx)[k], sel(cx.hb, nx)[k], cx.elab[e], pa, pb);
+              for (int q = (int)(pa & (uint64_t)(cx.hts - 1));; q = (q + 1) & (cx.hts - 1)) {
+                const int c = cx.htab[q];
+                if (c < 0) break;
+                if (sel(cx.ha, nx)[c] == pa && sel(cx.hb, nx)[c] == pb) { parent = c; break; }
+              }
+            }
+          }
+          npar[j] = parent;
+          nfl[j] = fl | (cx.eflg[e] & (F_HB | F_HN));
+        }
+      }
+      if constexpr (INPLACE) __syncthreads();
+#pragma unroll
+      for (int j = 0; j < KM; ++j) {
+        const int k = lane + 64 * j;
+        if (k < n) {
+          const int e = cx.sorted[k];
+          const uint32_t kd = cx.ekind[e];
+          const int ef = nfl[j];
+          sel(cx.lab, nx)[k] = cx.elab[e];
+          sel(cx.par, nx)[k] = npar[j];
+          sel(cx.flg, nx)[k] = ef;
+          sel(cx.ot, nx)[k] = cx.et[e]; sel(cx.ob, nx)[k] = cx.eb[e]; sel(cx.ol, nx)[k] = cx.el[e];
+          sel(cx.cb, nx)[k] = cx.ecb[e]; sel(cx.cn, nx)[k] = cx.ecn[e];
+          if constexpr (SC::kStateful) sel(cx.est, nx)[k] = cx.eest[e];
+          rout[k] = rec_pack(kd, cx.elab[e], (ef & F_HB) ? cx.ebpb[e] : kBpNone,
+                             (ef & F_HN) ? cx.ebpn[e] : kBpNone);
+        }
+      }
     }
     __syncthreads();
     buf = nx;

@@ -109,27 +109,32 @@ __host__ __device__ inline int htab_size(int W) {
 // LDS bytes needed by the decode kernel (host + device agree on the carve).
 constexpr size_t kLdsBytes = 160 * 1024;   // LDS per CU on gfx950 (one workgroup per item)
 
+// Large C (> 64, the BIG kernels): one buffer of branch arrays, which the
+// per-frame commit updates in place (the row of C values takes the room; two
+// items then fit one CU at cfg5).  C <= 64: two buffers, by frame parity.
+__host__ __device__ inline bool decode_inplace(int64_t C) { return C > 64; }
+
 // Bytes of the decode kernel's LDS layout for a beam capacity W (carve() in
 // ctcx_decode.hip, same order and alignment).
 __host__ __device__ inline size_t decode_lds_bytes(int W, int64_t C, int tsize, bool scored = false) {
   const size_t ENC = 3 * (size_t)W + 2;
+  const size_t nbuf = decode_inplace(C) ? 1 : 2;
   auto a16 = [](size_t v) { return (v + 15) & ~(size_t)15; };
   size_t s = 0;
-  s += 2 * a16(5 * (size_t)W * tsize);          // branch probs, 2 buffers
-  s += 2 * a16(3 * (size_t)W * 4);              // branch label/parent/flags, 2 buffers
+  s += nbuf * a16(5 * (size_t)W * tsize);       // branch probs
+  s += nbuf * a16(3 * (size_t)W * 4);           // branch label/parent/flags
   s += a16(4 * (size_t)W * 4);                  // child lists, state, new positions
   s += a16(5 * ENC * tsize);                    // entry probs
   s += a16(5 * ENC * 4);                        // entry bps/kind/label/flags
   s += a16(((size_t)W + 1) * 4) * 2;            // heap, top-paths scratch
-  s += a16(ENC * 4);                            // free list / slot map
   s += a16((size_t)W * 4);                      // sorted
   s += a16((size_t)W * 4);                      // alias (entries the beam holds twice)
   s += 64;                                      // scalars
-  s += 2 * 4 * (size_t)W * 8;                   // prefix hashes, 2 buffers
-  s += a16(4 * (size_t)htab_size(W));           // per-frame new-leaf hash table
-  s += a16(8 * (size_t)W);                      // per-branch evicted-child label bloom
+  s += nbuf * 2 * (size_t)W * 8;                // prefix hashes (two 64-bit chains)
+  s += a16(4 * (size_t)htab_size(W));           // per-frame new-leaf hash table  } the free list / slot
+  s += a16(8 * (size_t)W);                      // per-branch evicted-child bloom } map aliases these two
   s += ((size_t)(W > 256 ? W : W > 128 ? 256 : 128) + 2 + 64) * (tsize == 8 ? 16 : 8); // TopN elements (value, slot) + per-lane dummy slots
-  if (scored) s += a16((2 * (size_t)W + ENC) * tsize); // beam-scorer states (branches x2, entries)
+  if (scored) s += a16((nbuf * (size_t)W + ENC) * tsize); // beam-scorer states (branches, entries)
   s += a16((size_t)C * tsize);                  // logit row
   s += a16((size_t)((C + 63) / 64) * tsize);    // its per-64-label block maxima
   if (C > 64) {                                 // compacted chunk offers, child label bitmap + window summary, top set
