@@ -26,6 +26,9 @@ template <typename T>
 hipError_t launch_row_norm(const T* x, const int32_t* sl, T* norm, int64_t T_, int64_t B, int64_t C,
                            int64_t xstride, hipStream_t s);
 hipError_t launch_traceback(const TraceParams& tp, hipStream_t s);
+template <typename T>
+hipError_t launch_row_prep(const T* x, const int32_t* sl, char* prep, int64_t T_, int64_t B, int64_t C,
+                           int64_t xstride, int blank, hipStream_t s);
 hipError_t launch_scan(const int32_t* len, int64_t* off, int64_t* res, int64_t B, int P, hipStream_t s);
 hipError_t launch_pack(const PackParams& pp, hipStream_t s);
 }  // namespace ctcx
@@ -106,7 +109,7 @@ struct Dev {
   hipStream_t own_stream = nullptr;
   hipStream_t s = nullptr;   // stream of the current call
   hipEvent_t ev[4] = {};
-  DevBuf x, sl, norm, rec, item, top_pos, top_kind, logp, seq, len, phase, sctab;
+  DevBuf x, sl, norm, prep, rec, item, top_pos, top_kind, logp, seq, len, phase, sctab;
   int64_t lo = 0, nb = 0;    // this call's shard [lo, lo + nb)
 };
 
@@ -129,7 +132,7 @@ struct ctcext_decoder {
 static void release_dev(Dev& d) {
   (void)hipSetDevice(d.device);
   if (d.own_stream) (void)hipStreamSynchronize(d.own_stream);
-  DevBuf* bufs[] = {&d.x, &d.sl, &d.norm, &d.rec, &d.item, &d.top_pos, &d.top_kind, &d.logp,
+  DevBuf* bufs[] = {&d.x, &d.sl, &d.norm, &d.prep, &d.rec, &d.item, &d.top_pos, &d.top_kind, &d.logp,
                     &d.seq, &d.len, &d.phase, &d.sctab};
   for (DevBuf* b : bufs) b->release();
   for (auto& ev : d.ev)
@@ -360,8 +363,12 @@ static int enqueue_shard(ctcext_decoder* d, Dev& v, bool root, const ctcext_deco
   HIP_OR_FAIL(v.seq.ensure(4 * (size_t)(Bo * P * 2 * T_)));
   HIP_OR_FAIL(v.len.ensure(4 * (size_t)(Bo * P * 2)));
 
+  if (C > 64) HIP_OR_FAIL(v.prep.ensure(ctcx::prep_row_bytes(C, (int)sizeof(T)) * (size_t)(T_ * Bs)));
+
   if (prof) HIP_OR_FAIL(hipEventRecord(v.ev[0], s));
   HIP_OR_FAIL(ctcx::launch_row_norm<T>(x, sl, (T*)v.norm.p, T_, Bs, C, xstride, s));
+  // large C: the row facts the decode kernel reads per frame (parallel pre-pass)
+  HIP_OR_FAIL(ctcx::launch_row_prep<T>(x, sl, (char*)v.prep.p, T_, Bs, C, xstride, a->blank_index, s));
   if (prof) HIP_OR_FAIL(hipEventRecord(v.ev[1], s));
 
   ctcx::DecodeParams<T> p{};
@@ -378,6 +385,7 @@ static int enqueue_shard(ctcext_decoder* d, Dev& v, bool root, const ctcext_deco
   p.log_prob = (T*)v.logp.p;
   p.prof = nullptr;
   p.scorer_tab = nullptr;
+  p.prep = (const char*)v.prep.p;
   if (a->scorer == CTCEXT_SCORER_BIGRAM) {   // each device reads its own copy
     const size_t tb = (size_t)((C + 1) * C) * sizeof(T);
     HIP_OR_FAIL(v.sctab.ensure(tb));

@@ -190,6 +190,9 @@ struct Ctx {
   // beam-scorer state (a stateful scorer only): per branch [buf][i], per entry
   CTCX_LDS T* est[2]; CTCX_LDS T* eest;
   const T* sctab;      // the scorer's table (global memory)
+  // large C: this frame's row facts from ctcx_row_prep (RowHdr)
+  T rxmax, rxout;
+  int rbad, rns;
   int W, C, blank, enc, hts, wcap;
   int hdum;            // he index of lane 0's dummy store slot
 };
@@ -212,7 +215,7 @@ template <typename T>
 __host__ __device__ __forceinline__ CTCX_LDS uint64_t* row_cbm(const Ctx<T>& cx) {
   return (CTCX_LDS uint64_t*)(row_cq(cx) + 64);
 }
-// ... then the row's top set (float rows): values, label indices, 64 each
+// ... then the row's top set (float rows): values, label indices, kTopK each
 template <typename T>
 __host__ __device__ __forceinline__ CTCX_LDS float* row_topx(const Ctx<T>& cx) {
   const int nw = (cx.C - 1 + 63) / 64;
@@ -1555,110 +1558,6 @@ __device__ __forceinline__ void cq_children(const Ctx<T>& cx, int buf, int nb, i
 }
 constexpr int kGatherWin = 8;   // kept 64-label windows per batch of row reads in the gather
 
-// Large C, float rows: the row's top set S = the non-blank labels whose value
-// is >= tau, for the smallest tau that leaves at most 64 of them (bisection
-// on the order-preserving integer key of the float), written in label-index
-// order to row_topx (values) and the int array after it (label indices).
-// Returns |S|; xout = the largest value outside S (-inf: none).  An offer
-// bound (x - norm) + ot is monotone in x, so when it fails for xout it fails
-// for every label outside S, and S alone holds the branch's candidates.
-template <typename T>
-__device__ __forceinline__ int row_top_set(const Ctx<T>& cx, T& xout) {
-  if constexpr (sizeof(T) != 4) {
-    xout = pinf<T>();
-    return 0;
-  } else {
-    const int lane = threadIdx.x;
-    const int Cm1 = cx.C - 1, blank = cx.blank;
-    auto key = [](float v) {
-      const unsigned b = __float_as_uint(v);
-      return b ^ ((b >> 31) ? 0xFFFFFFFFu : 0x80000000u);
-    };
-    auto kat = [&](int x) { return key(cx.row[x + (x >= blank ? 1 : 0)]); };
-    constexpr int KR = 16;   // rows of up to 64 * KR labels keep their keys in registers
-    unsigned kr[KR];
-    const bool inreg = Cm1 <= 64 * KR;
-    unsigned lmax = 0u, lmaxx = 0u;   // the lane's largest key (rows > 64 * KR: over its stripe)
-#pragma unroll
-    for (int j = 0; j < KR; ++j) {
-      const int x = 64 * j + lane;
-      kr[j] = (inreg && x < Cm1) ? kat(x) : 0u;
-      lmax = kr[j] > lmax ? kr[j] : lmax;
-    }
-    if (!inreg) {
-#pragma unroll 8
-      for (int x = lane; x < Cm1; x += 64) {
-        const unsigned kx = kat(x);
-        lmaxx = kx > lmaxx ? kx : lmaxx;
-      }
-      lmax = lmaxx;
-    }
-    // |{key >= tau}|: each lane counts its own labels (no ballot per 64
-    // labels), then one bit-sliced wave sum (a lane counts at most 1024)
-    const int nbits = 32 - __builtin_clz((unsigned)((Cm1 + 63) / 64));
-    auto cnt_ge = [&](unsigned tau) {
-      int c = 0;
-      if (inreg) {
-#pragma unroll
-        for (int j = 0; j < KR; ++j) c += (kr[j] >= tau && 64 * j + lane < Cm1) ? 1 : 0;
-      } else {
-#pragma unroll 8
-        for (int x = lane; x < Cm1; x += 64) c += (kat(x) >= tau) ? 1 : 0;
-      }
-      int tot = 0;
-      for (int b = 0; b < nbits; ++b) tot += __builtin_popcountll(__ballot((c >> b) & 1)) << b;
-      return tot;
-    };
-    // smallest tau with |{key >= tau}| <= 64: cnt(lo) > 64 >= cnt(hi).  The
-    // answer's set S is that of the row's 64 largest values without a tie
-    // across the boundary, so any bracket with the invariant gives the same S.
-    // Bracket: hi = the row's largest key + 1; the smallest lane maximum km has
-    // at least 64 keys at or above it (one per lane), so cnt(km) >= 64: either
-    // exactly the 64 largest, or lo = km
-    uint64_t lo = 0, hi = 1ull << 32;
-    if (Cm1 <= 64) {
-      hi = 0;
-    } else {
-      hi = (uint64_t)(unsigned)uni((int)wave_max(lmax)) + 1ull;
-      const unsigned km = (unsigned)uni((int)wave_min(lmax));
-      const int c = cnt_ge(km);
-      if (c > 64) lo = km;
-      else hi = km;
-      if (c == 64) lo = hi;   // exactly the 64 largest
-    }
-    while (hi - lo > 1) {
-      const uint64_t mid = (lo + hi) >> 1;
-      const int c = cnt_ge((unsigned)mid);
-      if (c <= 64) hi = mid;
-      else lo = mid;
-      if (c == 64) break;
-    }
-    const unsigned tau = (unsigned)hi;
-    CTCX_LDS float* sx = row_topx(cx);
-    CTCX_LDS int* sli = (CTCX_LDS int*)(sx + 64);
-    float xo = ninf<float>();
-    int n = 0;
-    for (int x0 = 0; x0 < Cm1; x0 += 64) {
-      const int x = x0 + lane;
-      bool in = false;
-      if (x < Cm1) {
-        const float v = cx.row[x + (x >= blank ? 1 : 0)];
-        in = key(v) >= tau;
-        if (!in) xo = v > xo ? v : xo;
-      }
-      const uint64_t m = __ballot(in);
-      if (in) {
-        const int r = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-        sx[n + r] = cx.row[x + (x >= blank ? 1 : 0)];
-        sli[n + r] = x;
-      }
-      n += __builtin_popcountll(m);
-    }
-    xout = uni(wave_max(xo));
-    return n;
-  }
-}
-
 template <typename T, int RN, bool BIG, class SC>
 __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, bool last, int P, int* n_out,
                           int* n_leaves, uint64_t* pc) {
@@ -1672,29 +1571,25 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
 
   bool bad = !(norm > NI && norm < pinf<T>());
   T xmax = NI;
-  // large C: per 64-label block maxima of the row (bounds for window skipping
-  // in the grow loop below), stored after the row
+  // large C: the row's maximum, its NaN / +inf test and the per 64-label block
+  // maxima (bounds for window skipping in the grow loop below, in LDS after
+  // the row) come from the pre-pass (ctcx_row_prep, loaded with the row)
   CTCX_LDS T* bmax = row_bmax(cx);
   if constexpr (BIG) {   // BIG <=> C > 64
-    for (int k = 0; k * 64 < C; ++k) {
-      const int j = k * 64 + lane;
-      const T xv = j < C ? cx.row[j] : NI;
-      bad |= (xv != xv) || (xv == pinf<T>());
-      xmax = xv > xmax ? xv : xmax;
-      const T bm = wave_max(xv);
-      if (lane == 0) bmax[k] = bm;
-    }
+    bad |= cx.rbad != 0;
+    xmax = cx.rxmax;
   } else {
     for (int j = lane; j < C; j += 64) {
       const T xv = cx.row[j];
       bad |= (xv != xv) || (xv == pinf<T>());
       xmax = xv > xmax ? xv : xmax;
     }
+    xmax = wave_max(xmax);
   }
   if (__ballot(bad)) return 1;
   // max_l (x_l - norm): float rounding is monotone, so pmax + base bounds
   // every offer's score p + base computed the reference's way
-  const T pmax = wave_max(xmax) - norm;
+  const T pmax = xmax - norm;
 
   // roll (decoder.h:87-92) + recursion (decoder.h:95-143), lanes over branches
   for (int i = lane; i < nb; i += 64) {
@@ -1763,8 +1658,10 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
   // a closed turn found by the gather, the branch whose children the bitmap holds
   int cqn = 0, cq_i0 = 0, cq_l0 = 0, cbr = -1;
   bool gstop = false;
-  int tsn = -1;      // |S|, the row's top set (row_top_set; -1: not yet computed this frame)
-  T txo = NI;        // the largest value outside S
+  // |S|, the row's top set, and the largest value outside S (pre-pass; for
+  // double rows |S| = 0 and the S path below is never taken)
+  const int tsn = BIG ? cx.rns : 0;
+  const T txo = BIG ? cx.rxout : NI;
   while (i0 < nb && !stop) {
     if constexpr (RN == 1 && !BIG && sizeof(T) == 4 && !SC::kStateful) {
       if (st == kTopHeap && W >= 2) {
@@ -2002,12 +1899,8 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       T otb = NI, ot0 = NI;
       bool enter = true;   // at the gather's start or a branch's first offer
       const uint64_t tg0 = pc ? __builtin_amdgcn_s_memtime() : 0;
-      if (tsn < 0) {
-        tsn = row_top_set(cx, txo);
-        if (pc) pc[19] += __builtin_amdgcn_s_memtime() - tg0;
-      }
-      const T tsx = lane < tsn ? (T)row_topx(cx)[lane] : NI;                      // S in label-index order:
-      const int tsl = lane < tsn ? ((CTCX_LDS int*)(row_topx(cx) + 64))[lane] : Cm1;   // lane j its j-th
+      const T tsx = lane < tsn ? (T)row_topx(cx)[lane] : NI;                          // S in label-index order:
+      const int tsl = lane < tsn ? ((CTCX_LDS int*)(row_topx(cx) + kTopK))[lane] : Cm1;   // lane j its j-th
       while (cqn < 64) {
         const uint64_t te0 = pc ? __builtin_amdgcn_s_memtime() : 0;
         if (enter) {
@@ -2995,6 +2888,25 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     const T* xr = prm.x + ((int64_t)t * prm.xstride + b) * C;
     for (int j = lane; j < C; j += 64) cx.row[j] = xr[j];
     const T norm = prm.norm[(int64_t)t * B + b];
+    if constexpr (BIG) {
+      // the pre-pass record of row (t, b): header, block maxima, top set
+      const char* pr = prm.prep + ((int64_t)t * B + b) * (int64_t)prep_row_bytes(C, (int)sizeof(T));
+      const RowHdr<T> rh = *(const RowHdr<T>*)pr;
+      cx.rxmax = rh.xmax; cx.rxout = rh.xout; cx.rbad = rh.bad; cx.rns = rh.ns;
+      const T* pbm = (const T*)(pr + prep_bmax_offset((int)sizeof(T)));
+      CTCX_LDS T* bmx = row_bmax(cx);
+      for (int k = lane; k * 64 < C; k += 64) bmx[k] = pbm[k];
+      if constexpr (sizeof(T) == 4) {
+        const uint2* ptop = (const uint2*)(pr + prep_top_offset(C, 4));
+        CTCX_LDS float* sx = row_topx(cx);
+        CTCX_LDS int* sli = (CTCX_LDS int*)(sx + kTopK);
+        for (int q = lane; q < rh.ns; q += 64) {
+          const uint2 e = ptop[q];
+          sx[q] = __uint_as_float(e.x);
+          sli[q] = (int)e.y;
+        }
+      }
+    }
     __syncthreads();
     const bool last = (t == sl - 1);
 
@@ -3263,6 +3175,112 @@ __global__ __launch_bounds__(64) void ctcx_row_norm(const T* __restrict__ x, con
 
 #if CTCX_PART == 0
 // ---------------------------------------------------------------------------
+// Large C (> 64): the row facts the decode kernel needs per frame (RowHdr,
+// block maxima, top set S; ctcx_kernels.h), for every (t, b) row, one wave
+// per row.  Fully parallel over rows: inside the decode kernel the same work
+// sat on the one-wave T-serial chain (at C=5000 the top-set bisection alone
+// took ~108k cycles per frame there).
+//   * block maxima: 64 classes per step, one wave max each, in class order;
+//   * S: bisection on the order-preserving integer key of the float for the
+//     smallest tau with |{non-blank x : key >= tau}| <= kTopK; any bracket
+//     keeping cnt(lo) > kTopK >= cnt(hi) yields the same S (the row's kTopK
+//     largest values without a tie across the boundary); the keys are staged
+//     in LDS when the row fits (kPrepLdsClasses), else re-read from global
+//     memory.
+// Rows past an item's length are skipped (never read).
+constexpr int kPrepLdsClasses = 16384;
+
+__device__ __forceinline__ unsigned fkey(float v) {
+  const unsigned u = __float_as_uint(v);
+  return u ^ ((u >> 31) ? 0xFFFFFFFFu : 0x80000000u);
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void ctcx_row_prep(const T* __restrict__ x, const int32_t* __restrict__ seq_len,
+                                                   char* __restrict__ prep, int64_t B, int64_t C, int64_t xstride,
+                                                   int blank) {
+  extern __shared__ __attribute__((aligned(16))) unsigned pkeys[];   // float rows: keys by class
+  const int lane = threadIdx.x;
+  const int64_t row = blockIdx.x;
+  const int64_t t = row / B, b = row - t * B;
+  if (t >= seq_len[b]) return;
+  const T NI = ninf<T>();
+  const T* xr = x + (t * xstride + b) * C;
+  char* pr = prep + row * (int64_t)prep_row_bytes(C, (int)sizeof(T));
+  T* bm = (T*)(pr + prep_bmax_offset((int)sizeof(T)));
+  const int nblk = (int)((C + 63) / 64);
+  const bool inlds = sizeof(T) == 4 && C <= kPrepLdsClasses;
+  T xmax = NI, bmv = NI;
+  bool bad = false;
+  for (int k = 0; k < nblk; ++k) {
+    const int j = k * 64 + lane;
+    const T xv = j < C ? xr[j] : NI;
+    bad |= (xv != xv) || (xv == pinf<T>());
+    xmax = xv > xmax ? xv : xmax;
+    const T m = wave_max(xv);
+    bmv = (lane == (k & 63)) ? m : bmv;
+    if ((k & 63) == 63 || k == nblk - 1) {
+      if (lane <= (k & 63)) bm[(k & ~63) + lane] = bmv;
+    }
+    if constexpr (sizeof(T) == 4) {
+      if (inlds && j < C) pkeys[j] = fkey((float)xv);
+    }
+  }
+  RowHdr<T> h;
+  h.xmax = wave_max(xmax);
+  h.bad = __ballot(bad) != 0ull;
+  h.ns = 0;
+  h.xout = pinf<T>();
+  if constexpr (sizeof(T) == 4) {
+    const int Cm1 = (int)C - 1;
+    auto kat = [&](int j) -> unsigned { return inlds ? pkeys[j] : fkey(xr[j]); };
+    // |{non-blank labels with key >= tau}|: per-lane counts, then one wave sum
+    auto cnt_ge = [&](unsigned tau) {
+      int c = 0;
+      for (int j = lane; j < (int)C; j += 64) c += (j != blank && kat(j) >= tau) ? 1 : 0;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o);
+      return uni(c);
+    };
+    uint64_t lo = 0, hi = 0;
+    if (Cm1 > kTopK) {
+      hi = (uint64_t)fkey((float)h.xmax) + 1ull;   // cnt(hi) = 0; cnt(lo = 0) = Cm1 > kTopK
+      while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) >> 1;
+        const int c = cnt_ge((unsigned)mid);
+        if (c <= kTopK) hi = mid;
+        else lo = mid;
+        if (c == kTopK) break;
+      }
+    }
+    const unsigned tau = (unsigned)hi;
+    uint2* top = (uint2*)(pr + prep_top_offset(C, 4));
+    float xo = ninf<float>();
+    int n = 0;
+    for (int x0 = 0; x0 < Cm1; x0 += 64) {
+      const int xi = x0 + lane;
+      bool in = false;
+      float v = 0.f;
+      if (xi < Cm1) {
+        const int j = xi + (xi >= blank ? 1 : 0);
+        v = (float)xr[j];
+        in = fkey(v) >= tau;
+        if (!in) xo = v > xo ? v : xo;
+      }
+      const uint64_t m = __ballot(in);
+      if (in) {
+        const int r = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+        top[n + r] = make_uint2(__float_as_uint(v), (unsigned)xi);
+      }
+      n += __builtin_popcountll(m);
+    }
+    h.ns = n;
+    h.xout = (T)wave_max(xo);
+  }
+  if (lane == 0) *(RowHdr<T>*)pr = h;
+}
+
+// ---------------------------------------------------------------------------
 // Backward walks over the records.  which = 0: decoded labels (LabelSeq,
 // ctc_beam_entry.h:123-136); which = 1: best alignment (AlignmentLabelSeq +
 // the candidate chain, ctc_beam_entry.h:137-152, 190-228).  Output reversed.
@@ -3480,6 +3498,25 @@ hipError_t launch_decode(const DecodeParams<T>& p, hipStream_t s) {
 
 template hipError_t launch_decode<float>(const DecodeParams<float>&, hipStream_t);
 template hipError_t launch_decode<double>(const DecodeParams<double>&, hipStream_t);
+
+template <typename T>
+hipError_t launch_row_prep(const T* x, const int32_t* sl, char* prep, int64_t T_, int64_t B, int64_t C,
+                           int64_t xstride, int blank, hipStream_t s) {
+  const int64_t rows = T_ * B;
+  if (rows == 0 || C <= 64) return hipSuccess;
+  const size_t lds = (sizeof(T) == 4 && C <= kPrepLdsClasses) ? (size_t)C * 4 : 0;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)ctcx_row_prep<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(ctcx_row_prep<T>, dim3((unsigned)rows), dim3(64), lds, s, x, sl, prep, B, C, xstride, blank);
+  return hipGetLastError();
+}
+template hipError_t launch_row_prep<float>(const float*, const int32_t*, char*, int64_t, int64_t, int64_t, int64_t,
+                                           int, hipStream_t);
+template hipError_t launch_row_prep<double>(const double*, const int32_t*, char*, int64_t, int64_t, int64_t, int64_t,
+                                            int, hipStream_t);
 
 template <typename T>
 hipError_t launch_row_norm(const T* x, const int32_t* sl, T* norm, int64_t T_, int64_t B, int64_t C,

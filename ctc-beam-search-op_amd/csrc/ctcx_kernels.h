@@ -58,6 +58,34 @@ struct ItemOut {
   int32_t pad[3];
 };
 
+// Large C (> 64): per-(t, b) row facts computed by the parallel pre-pass
+// ctcx_row_prep before the decode kernel, which would otherwise derive them
+// inside its T-serial chain (one wave per item): the row maximum, whether it
+// holds a NaN / +inf, the maxima of its 64-class blocks, and (float rows) the
+// row's top set S -- the non-blank labels whose value is >= tau for the
+// smallest tau leaving at most kTopK of them -- in label-index order, with the
+// largest value outside S.  All depend on x[t, b, :] only.
+constexpr int kTopK = 64;
+template <typename T>
+struct RowHdr {
+  T xmax;       // max over the row's C values
+  T xout;       // largest non-blank value outside S (-inf: none; +inf: no top set)
+  int32_t bad;  // the row holds a NaN or +inf
+  int32_t ns;   // |S|
+};
+// One row's record: RowHdr, the nblk block maxima (T), then S as kTopK
+// (float value, int32 label index) pairs (float rows only); 16-byte aligned.
+__host__ __device__ inline size_t prep_row_bytes(int64_t C, int tsize) {
+  const size_t hdr = tsize == 4 ? 16 : 32;
+  size_t s = hdr + ((((size_t)(C + 63) / 64) * tsize + 15) & ~(size_t)15);
+  if (tsize == 4) s += (size_t)kTopK * 8;
+  return s;
+}
+__host__ __device__ inline size_t prep_bmax_offset(int tsize) { return tsize == 4 ? 16 : 32; }
+__host__ __device__ inline size_t prep_top_offset(int64_t C, int tsize) {
+  return prep_bmax_offset(tsize) + ((((size_t)(C + 63) / 64) * tsize + 15) & ~(size_t)15);
+}
+
 template <typename T>
 struct DecodeParams {
   const T* x;               // row (t, b) at x + (t * xstride + b) * C
@@ -74,6 +102,7 @@ struct DecodeParams {
   T* log_prob;              // [B][P]
   uint64_t* prof;           // optional [B][8] phase cycle counters (diagnostics)
   const T* scorer_tab;      // bigram beam-scorer table [C + 1][C], or null (BaseBeamScorer)
+  const char* prep;         // C > 64: [Tmax][B] row records of ctcx_row_prep (prep_row_bytes each)
 };
 
 struct TraceParams {
@@ -139,7 +168,7 @@ __host__ __device__ inline size_t decode_lds_bytes(int W, int64_t C, int tsize, 
   s += a16((size_t)((C + 63) / 64) * tsize);    // its per-64-label block maxima
   if (C > 64) {                                 // compacted chunk offers, child label bitmap + window summary, top set
     const size_t nw = (size_t)(C - 1 + 63) / 64;
-    s += 64 * 4 + 8 * nw + 8 * ((nw + 63) / 64) + 64 * 8;   // + the row's top set (value, label index) x 64
+    s += 64 * 4 + 8 * nw + 8 * ((nw + 63) / 64) + (size_t)kTopK * 8;   // + the row's top set (value, label index)
   }
   return s;
 }
