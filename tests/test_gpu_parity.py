@@ -384,6 +384,18 @@ def test_random_large_c_compacted():
     _run_random(894, 8, T_max=40, B_max=2, C_min=300, C_max=1200, W_min=64, W_max=256, scale=2.5)
 
 
+def test_random_large_c_top_set():
+    # the row's top set S (ctcx_row_prep, 64 labels): C just above it makes S a
+    # strict subset; flat rows (small scale) and wide beams give top branches
+    # more hot offers than S holds (the window path takes over) and many
+    # branch children to merge; ties put equal values at the threshold and in
+    # S; C above 2048 (a wider S was tried there)
+    _run_random(911, 10, T_max=30, B_max=2, C_min=66, C_max=200, W_min=100, W_max=256, scale=0.3)
+    _run_random(912, 6, T_max=16, B_max=2, C_min=2049, C_max=2400, W_min=100, W_max=256, scale=0.3)
+    _run_random(913, 6, T_max=16, B_max=2, C_min=2049, C_max=2200, W_min=20, W_max=200, ties=True)
+    _run_random(914, 4, T_max=24, B_max=2, C_min=2049, C_max=4000, W_min=64, W_max=256, scale=0.5)
+
+
 def test_random_wide_beam_events():
     # beams of 129..256 (float): the two-group asm event loop (heap_events_m2_f32)
     # with the stop in either group, small C (64-offer chunks) and large C
