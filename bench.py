@@ -183,7 +183,8 @@ def strong_scaling(args, cfg, world, rank, dev, dec, gather_to_root):
         el = float(el.item())
         return {"global_batch": B, "batch_per_gpu": nb, "n_gpus": world, "steps": steps,
                 "frames_per_s": B * T * steps / el, "ms_per_step": 1e3 * el / steps,
-                "what": "measured: fixed global batch split over the ranks, RCCL gather to rank 0"}
+                "what": "measured: fixed global batch split over the ranks, %s gather to rank 0"
+                        % ("RCCL" if dist.get_backend() == "nccl" else dist.get_backend())}
     proj = []
     for n in (1, 2, 4, 8):
         nb = B // n
@@ -339,7 +340,8 @@ def main():
         "literal_frames_per_step": lit / max(args.steps, 1),
         "lib_sha16": lib_hash(),
         "what": ("one decode call: device logits in, int64 SparseTensor components materialised on the host"
-                 if world == 1 else "one decode call per rank (device outputs) + RCCL gather to rank 0"),
+                 if world == 1 else "one decode call per rank (device outputs) + %s gather to rank 0"
+                 % ("RCCL" if backend == "nccl" else backend)),
     }
     if world == 1 and not args.no_host_io:
         # the same call with the components left in HBM (no device->host copy)
