@@ -32,6 +32,8 @@ hipError_t launch_row_prep(const T* x, const int32_t* sl, char* prep, int64_t T_
 hipError_t launch_scan(const int32_t* len, int64_t* off, int64_t* res, int64_t B, int P, hipStream_t s);
 hipError_t launch_pack(const PackParams& pp, hipStream_t s);
 }  // namespace ctcx
+// the global-state tier (ctcx_decode.hip compiled with CTCX_GSTATE)
+hipError_t ctcx_gstate_launch_decode(const void* p, int is_f64, int scored, hipStream_t s);
 
 static thread_local std::string g_err;
 
@@ -109,7 +111,7 @@ struct Dev {
   hipStream_t own_stream = nullptr;
   hipStream_t s = nullptr;   // stream of the current call
   hipEvent_t ev[4] = {};
-  DevBuf x, sl, norm, prep, rec, item, top_pos, top_kind, logp, seq, len, phase, sctab;
+  DevBuf x, sl, norm, prep, rec, item, top_pos, top_kind, logp, seq, len, phase, sctab, gstate;
   int64_t lo = 0, nb = 0;    // this call's shard [lo, lo + nb)
 };
 
@@ -133,7 +135,7 @@ static void release_dev(Dev& d) {
   (void)hipSetDevice(d.device);
   if (d.own_stream) (void)hipStreamSynchronize(d.own_stream);
   DevBuf* bufs[] = {&d.x, &d.sl, &d.norm, &d.prep, &d.rec, &d.item, &d.top_pos, &d.top_kind, &d.logp,
-                    &d.seq, &d.len, &d.phase, &d.sctab};
+                    &d.seq, &d.len, &d.phase, &d.sctab, &d.gstate};
   for (DevBuf* b : bufs) b->release();
   for (auto& ev : d.ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -141,12 +143,18 @@ static void release_dev(Dev& d) {
   d.own_stream = nullptr;
 }
 
+// The LDS-resident fast tier: the 8-byte record's limits and the LDS carve.
 static int32_t max_beam_width(int64_t num_classes, int32_t dtype, bool scored) {
   const int ts = dtype == CTCEXT_F64 ? 8 : 4;
+  if (num_classes > ctcx::kMaxRecClasses) return 0;
   int lo = 0;
-  for (int w = 1; w <= 512; ++w)
+  for (int w = 1; w <= ctcx::kMaxRecBeam; ++w)
     if (ctcx::decode_lds_bytes(w, num_classes, ts, scored) <= ctcx::kLdsBytes) lo = w;
   return lo;
+}
+static bool use_gstate(const ctcext_decode_args* a) {
+  return (a->flags & CTCEXT_FLAG_GLOBAL_STATE) ||
+         a->beam_width > max_beam_width(a->num_classes, a->dtype, a->scorer != CTCEXT_SCORER_BASE);
 }
 
 extern "C" int32_t ctcext_max_beam_width(int64_t num_classes, int32_t dtype) {
@@ -292,15 +300,10 @@ static int check_limits(const ctcext_decode_args* a) {
     return fail(CTCEXT_INVALID_ARGUMENT, "blank_index out of range [0, num_classes)");
   // decoder.h:237-239 — raised by the first item's TopPaths
   if (a->top_paths > a->beam_width) return fail(CTCEXT_INVALID_ARGUMENT, "requested more paths than the beam width.");
-  if (C > ctcx::kMaxRecClasses)
-    return fail(CTCEXT_UNIMPLEMENTED, "num_classes " + std::to_string(C) +
-                                          " exceeds the back-pointer record format (max " +
-                                          std::to_string(ctcx::kMaxRecClasses) + ")");
-  const int wmax = max_beam_width(C, a->dtype, a->scorer != CTCEXT_SCORER_BASE);
-  if (a->beam_width > wmax)
-    return fail(CTCEXT_UNIMPLEMENTED, "beam_width " + std::to_string(a->beam_width) + " with num_classes " +
-                                          std::to_string(C) + " exceeds the LDS-resident beam state (max " +
-                                          std::to_string(wmax) + ")");
+  // every shape decodes (the global-state tier takes what the LDS tier cannot);
+  // this library's int32 positions and labels bound it
+  if (C > INT32_MAX / 2 || a->beam_width > (1 << 28))
+    return fail(CTCEXT_UNIMPLEMENTED, "num_classes or beam_width beyond this library's 32-bit indices");
   return CTCEXT_OK;
 }
 
@@ -363,12 +366,20 @@ static int enqueue_shard(ctcext_decoder* d, Dev& v, bool root, const ctcext_deco
   HIP_OR_FAIL(v.seq.ensure(4 * (size_t)(Bo * P * 2 * T_)));
   HIP_OR_FAIL(v.len.ensure(4 * (size_t)(Bo * P * 2)));
 
-  if (C > 64) HIP_OR_FAIL(v.prep.ensure(ctcx::prep_row_bytes(C, (int)sizeof(T)) * (size_t)(T_ * Bs)));
+  const bool gs = use_gstate(a);
+  const bool scored = a->scorer != CTCEXT_SCORER_BASE;
+  if (gs) {
+    // the global-state tier: 16-byte records, the beam state in HBM
+    HIP_OR_FAIL(v.rec.ensure(sizeof(ctcx::Rec16) * (size_t)(Bs * T_ * W)));
+    HIP_OR_FAIL(v.gstate.ensure(ctcx::gstate_bytes(W, (int)sizeof(T), scored) * (size_t)Bs));
+  } else if (C > 64) {
+    HIP_OR_FAIL(v.prep.ensure(ctcx::prep_row_bytes(C, (int)sizeof(T)) * (size_t)(T_ * Bs)));
+  }
 
   if (prof) HIP_OR_FAIL(hipEventRecord(v.ev[0], s));
   HIP_OR_FAIL(ctcx::launch_row_norm<T>(x, sl, (T*)v.norm.p, T_, Bs, C, xstride, s));
   // large C: the row facts the decode kernel reads per frame (parallel pre-pass)
-  HIP_OR_FAIL(ctcx::launch_row_prep<T>(x, sl, (char*)v.prep.p, T_, Bs, C, xstride, a->blank_index, s));
+  if (!gs) HIP_OR_FAIL(ctcx::launch_row_prep<T>(x, sl, (char*)v.prep.p, T_, Bs, C, xstride, a->blank_index, s));
   if (prof) HIP_OR_FAIL(hipEventRecord(v.ev[1], s));
 
   ctcx::DecodeParams<T> p{};
@@ -397,15 +408,22 @@ static int enqueue_shard(ctcext_decoder* d, Dev& v, bool root, const ctcext_deco
     p.prof = (uint64_t*)v.phase.p;
   }
   // the host checked the shapes the kernel's grid and LDS carve assume
-  if (Bs > 0x7fffffffLL || W > 512 || C > ctcx::kMaxRecClasses)
+  if (Bs > 0x7fffffffLL || (!gs && (W > ctcx::kMaxRecBeam || C > ctcx::kMaxRecClasses)))
     return fail(CTCEXT_INTERNAL, "shard shape outside the kernel's limits");
-  HIP_OR_FAIL(ctcx::launch_decode<T>(p, s));
+  if (gs) {
+    p.gstate = (char*)v.gstate.p;
+    p.gstate_stride = (int64_t)ctcx::gstate_bytes(W, (int)sizeof(T), scored);
+    HIP_OR_FAIL(ctcx_gstate_launch_decode(&p, sizeof(T) == 8, scored, s));
+  } else {
+    HIP_OR_FAIL(ctcx::launch_decode<T>(p, s));
+  }
   if (prof) HIP_OR_FAIL(hipEventRecord(v.ev[2], s));
 
   ctcx::TraceParams tp{};
   tp.rec = p.rec; tp.item = p.item; tp.seq_len = sl; tp.top_pos = p.top_pos; tp.top_kind = p.top_kind;
   tp.Tmax = T_; tp.B = Bs; tp.W = W; tp.P = P; tp.merge = a->merge_repeated ? 1 : 0;
   tp.blank_label = a->blank_label;
+  tp.rec_wide = gs ? 1 : 0;
   tp.seq = (int32_t*)v.seq.p;
   tp.len = (int32_t*)v.len.p;
   tp.len_stride = Bo;
@@ -506,6 +524,7 @@ static int run_decode(ctcext_decoder* d, const ctcext_decode_args* a, const std:
   HIP_OR_FAIL(hipStreamSynchronize(s));
 
   d->stats = ctcext_stats{};
+  d->stats.tier = use_gstate(a) ? 1 : 0;
   if (a->flags & CTCEXT_FLAG_PROFILE) {
     for (int i = 0; i < nd; ++i) {
       Dev& v = d->devs[(size_t)i];

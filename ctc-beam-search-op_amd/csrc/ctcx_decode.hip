@@ -2838,9 +2838,16 @@ __host__ __device__ __attribute__((noinline)) int literal_step(Ctx<T> cx, int bu
 // ---------------------------------------------------------------------------
 template <typename T, int RN, int WC, bool BIG, class SC>
 __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
   Ctx<T> cx;
+#ifdef CTCX_GSTATE
+  // global-state tier: the item's state in global memory (gstate_bytes), the
+  // row read in place from the inputs
+  carve(cx, prm.gstate + (int64_t)blockIdx.x * prm.gstate_stride, prm.W, prm.W, 1, SC::kStateful, false);
+  cx.C = (int)prm.C;
+#else
+  extern __shared__ __attribute__((aligned(16))) char lds[];
   carve(cx, (CTCX_LDS char*)lds, WC > 0 ? WC : prm.W, prm.W, (int)prm.C, SC::kStateful, BIG);   // BIG == decode_inplace(C)
+#endif
   cx.blank = prm.blank;
   cx.sctab = prm.scorer_tab;
   const int lane = threadIdx.x;
@@ -2886,7 +2893,11 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
   for (int t = 0; t < sl; ++t) {
     uint64_t t0 = prof ? __builtin_amdgcn_s_memtime() : 0;
     const T* xr = prm.x + ((int64_t)t * prm.xstride + b) * C;
+#ifdef CTCX_GSTATE
+    cx.row = const_cast<T*>(xr);
+#else
     for (int j = lane; j < C; j += 64) cx.row[j] = xr[j];
+#endif
     const T norm = prm.norm[(int64_t)t * B + b];
     if constexpr (BIG) {
       // the pre-pass record of row (t, b): header, block maxima, top set
@@ -2915,8 +2926,10 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     int nl_fast = 0;
     uint64_t t1 = prof ? __builtin_amdgcn_s_memtime() : 0;
     if (prof) pc[0] += t1 - t0;
+#ifndef CTCX_GSTATE   // the global-state tier replays every frame literally
     if (!prm.force_literal && !dup)
       why = exact_step<T, RN, BIG, SC>(cx, buf, nb, norm, last, prm.P, &n, &nl_fast, prof ? pc : nullptr);
+#endif
     __syncthreads();
     uint64_t t2 = prof ? __builtin_amdgcn_s_memtime() : 0;
     const bool ok = (why == 0);
@@ -2961,97 +2974,108 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     }
     for (int q = lane; q < cx.hts; q += 64) cx.htab[q] = -1;
     __syncthreads();
-    // prefix hashes of the new leaves; new children go into the hash table
-    {
+    // One position k of the commit: the new prefix hash (phase 1), then the
+    // parent position and flags (phase 2), then the writes.  In place (large
+    // C), every read of the frame-start arrays precedes every write (staged in
+    // registers, KM positions per lane, W <= 512 on that tier); double
+    // buffered, each position is read and written in one pass (any W).
+    auto hash_of = [&](int k, uint64_t& ha, uint64_t& hb) {
+      const int e = cx.sorted[k];
+      const uint32_t kd = cx.ekind[e];
+      const int src = (int)(kd >> 1);
+      ha = sel(cx.ha, buf)[src];
+      hb = sel(cx.hb, buf)[src];
+      if (kd & 1u) hmix(ha, hb, cx.elab[e], ha, hb);
+    };
+    auto put_hash = [&](int k, uint64_t ha, uint64_t hb) {
+      sel(cx.ha, nx)[k] = ha;
+      sel(cx.hb, nx)[k] = hb;
+      if ((cx.ekind[cx.sorted[k]] & 1u) && (!dup_next || cx.alias[k] == k)) {
+        int q = (int)(ha & (uint64_t)(cx.hts - 1));
+        int expect = -1;
+        while (!__hip_atomic_compare_exchange_strong(&cx.htab[q], &expect, k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP)) {
+          q = (q + 1) & (cx.hts - 1);
+          expect = -1;
+        }
+      }
+    };
+    auto parent_of = [&](int k, int& parent, int& fl) {
+      const int e = cx.sorted[k];
+      const uint32_t kd = cx.ekind[e];
+      const int src = (int)(kd >> 1);
+      const int pf = sel(cx.flg, buf)[src];
+      if (kd & 1u) {
+        parent = cx.newpos[src];
+        fl = (pf & F_ROOT) ? F_PROOT : 0;
+      } else {
+        const int pp = sel(cx.par, buf)[src];
+        parent = pp >= 0 ? cx.newpos[pp] : -1;
+        fl = pf & (F_ROOT | F_PROOT);
+        if (pp < 0 && !(pf & F_ROOT)) {
+          // the parent node was not in the beam; it may have re-entered this
+          // frame as a new child (the reference finds it through the trie)
+          uint64_t pa, pb;
+          hmix_inv(sel(cx.ha, nx)[k], sel(cx.hb, nx)[k], cx.elab[e], pa, pb);
+          for (int q = (int)(pa & (uint64_t)(cx.hts - 1));; q = (q + 1) & (cx.hts - 1)) {
+            const int c = cx.htab[q];
+            if (c < 0) break;
+            if (sel(cx.ha, nx)[c] == pa && sel(cx.hb, nx)[c] == pb) { parent = c; break; }
+          }
+        }
+      }
+      fl |= cx.eflg[e] & (F_HB | F_HN);
+    };
+    auto put_branch = [&](int k, int parent, int ef) {
+      const int e = cx.sorted[k];
+      const uint32_t kd = cx.ekind[e];
+      sel(cx.lab, nx)[k] = cx.elab[e];
+      sel(cx.par, nx)[k] = parent;
+      sel(cx.flg, nx)[k] = ef;
+      sel(cx.ot, nx)[k] = cx.et[e]; sel(cx.ob, nx)[k] = cx.eb[e]; sel(cx.ol, nx)[k] = cx.el[e];
+      sel(cx.cb, nx)[k] = cx.ecb[e]; sel(cx.cn, nx)[k] = cx.ecn[e];
+      if constexpr (SC::kStateful) sel(cx.est, nx)[k] = cx.eest[e];
+      const uint32_t bpb = (ef & F_HB) ? cx.ebpb[e] : kBpNone, bpn = (ef & F_HN) ? cx.ebpn[e] : kBpNone;
+#ifdef CTCX_GSTATE
+      ((Rec16*)prm.rec)[((int64_t)b * prm.Tmax + t) * W + k] = Rec16{kd, cx.elab[e], bpb, bpn};
+#else
+      prm.rec[((int64_t)b * prm.Tmax + t) * W + k] = rec_pack(kd, cx.elab[e], bpb, bpn);
+#endif
+    };
+    if constexpr (INPLACE) {
       uint64_t nha[KM], nhb[KM];
 #pragma unroll
       for (int j = 0; j < KM; ++j) {
-        const int k = lane + 64 * j;
         nha[j] = nhb[j] = 0;
-        if (k < n) {
-          const int e = cx.sorted[k];
-          const uint32_t kd = cx.ekind[e];
-          const int src = (int)(kd >> 1);
-          nha[j] = sel(cx.ha, buf)[src];
-          nhb[j] = sel(cx.hb, buf)[src];
-          if (kd & 1u) hmix(nha[j], nhb[j], cx.elab[e], nha[j], nhb[j]);
-        }
+        if (lane + 64 * j < n) hash_of(lane + 64 * j, nha[j], nhb[j]);
       }
-      if constexpr (INPLACE) __syncthreads();
+      __syncthreads();
 #pragma unroll
-      for (int j = 0; j < KM; ++j) {
-        const int k = lane + 64 * j;
-        if (k < n) {
-          sel(cx.ha, nx)[k] = nha[j];
-          sel(cx.hb, nx)[k] = nhb[j];
-          if ((cx.ekind[cx.sorted[k]] & 1u) && (!dup_next || cx.alias[k] == k)) {
-            int q = (int)(nha[j] & (uint64_t)(cx.hts - 1));
-            int expect = -1;
-            while (!__hip_atomic_compare_exchange_strong(&cx.htab[q], &expect, k, __ATOMIC_RELAXED,
-                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-              q = (q + 1) & (cx.hts - 1);
-              expect = -1;
-            }
-          }
-        }
-      }
-    }
-    __syncthreads();
-    Rec* rout = prm.rec + ((int64_t)b * prm.Tmax + t) * W;
-    {
+      for (int j = 0; j < KM; ++j)
+        if (lane + 64 * j < n) put_hash(lane + 64 * j, nha[j], nhb[j]);
+      __syncthreads();
       int npar[KM], nfl[KM];
 #pragma unroll
       for (int j = 0; j < KM; ++j) {
-        const int k = lane + 64 * j;
         npar[j] = -1;
         nfl[j] = 0;
-        if (k < n) {
-          const int e = cx.sorted[k];
-          const uint32_t kd = cx.ekind[e];
-          const int src = (int)(kd >> 1);
-          const bool isnew = (kd & 1u) != 0;
-          const int pf = sel(cx.flg, buf)[src];
-          int parent, fl;
-          if (isnew) {
-            parent = cx.newpos[src];
-            fl = (pf & F_ROOT) ? F_PROOT : 0;
-          } else {
-            const int pp = sel(cx.par, buf)[src];
-            parent = pp >= 0 ? cx.newpos[pp] : -1;
-            fl = pf & (F_ROOT | F_PROOT);
-            if (pp < 0 && !(pf & F_ROOT)) {
-              // the parent node was not in the beam; it may have re-entered this
-              // frame as a new child (the reference finds it through the trie)
-              uint64_t pa, pb;
-              hmix_inv(sel(cx.ha, nx)[k], sel(cx.hb, nx)[k], cx.elab[e], pa, pb);
-              for (int q = (int)(pa & (uint64_t)(cx.hts - 1));; q = (q + 1) & (cx.hts - 1)) {
-                const int c = cx.htab[q];
-                if (c < 0) break;
-                if (sel(cx.ha, nx)[c] == pa && sel(cx.hb, nx)[c] == pb) { parent = c; break; }
-              }
-            }
-          }
-          npar[j] = parent;
-          nfl[j] = fl | (cx.eflg[e] & (F_HB | F_HN));
-        }
+        if (lane + 64 * j < n) parent_of(lane + 64 * j, npar[j], nfl[j]);
       }
-      if constexpr (INPLACE) __syncthreads();
+      __syncthreads();
 #pragma unroll
-      for (int j = 0; j < KM; ++j) {
-        const int k = lane + 64 * j;
-        if (k < n) {
-          const int e = cx.sorted[k];
-          const uint32_t kd = cx.ekind[e];
-          const int ef = nfl[j];
-          sel(cx.lab, nx)[k] = cx.elab[e];
-          sel(cx.par, nx)[k] = npar[j];
-          sel(cx.flg, nx)[k] = ef;
-          sel(cx.ot, nx)[k] = cx.et[e]; sel(cx.ob, nx)[k] = cx.eb[e]; sel(cx.ol, nx)[k] = cx.el[e];
-          sel(cx.cb, nx)[k] = cx.ecb[e]; sel(cx.cn, nx)[k] = cx.ecn[e];
-          if constexpr (SC::kStateful) sel(cx.est, nx)[k] = cx.eest[e];
-          rout[k] = rec_pack(kd, cx.elab[e], (ef & F_HB) ? cx.ebpb[e] : kBpNone,
-                             (ef & F_HN) ? cx.ebpn[e] : kBpNone);
-        }
+      for (int j = 0; j < KM; ++j)
+        if (lane + 64 * j < n) put_branch(lane + 64 * j, npar[j], nfl[j]);
+    } else {
+      for (int k = lane; k < n; k += 64) {
+        uint64_t ha, hb;
+        hash_of(k, ha, hb);
+        put_hash(k, ha, hb);
+      }
+      __syncthreads();
+      for (int k = lane; k < n; k += 64) {
+        int parent, fl;
+        parent_of(k, parent, fl);
+        put_branch(k, parent, fl);
       }
     }
     __syncthreads();
@@ -3297,14 +3321,24 @@ __global__ __launch_bounds__(256) void ctcx_traceback(TraceParams tp) {
   int len = 0;
   int k = tp.top_pos[bp];
   if (sl > 0 && k >= 0 && p < tp.item[b].n_leaves) {
-    const Rec* rb = tp.rec + b * tp.Tmax * tp.W;
+    // record (t, k) unpacked: link, label, the two alignment back-pointers
+    auto rd = [&](int t, uint32_t& link, int& lab, uint32_t& bpb, uint32_t& bpn) {
+      const int64_t at = (b * tp.Tmax + t) * tp.W + k;
+      if (tp.rec_wide) {
+        const Rec16 r = ((const Rec16*)tp.rec)[at];
+        link = r.link; lab = r.label; bpb = r.bpb; bpn = r.bpn;
+      } else {
+        const Rec r = tp.rec[at];
+        link = rec_link(r); lab = rec_label(r); bpb = rec_bp_blank(r); bpn = rec_bp_nblank(r);
+      }
+    };
     if (which == 0) {
       int prev = -1;
       for (int t = sl - 1; t >= 0; --t) {
-        const Rec r = rb[(int64_t)t * tp.W + k];
-        const uint32_t link = rec_link(r);
+        uint32_t link, bpb, bpn;
+        int lab;
+        rd(t, link, lab, bpb, bpn);
         if (link & 1u) {
-          const int lab = rec_label(r);
           if (!tp.merge || lab != prev) out[len++] = lab;
           prev = lab;
         }
@@ -3313,9 +3347,11 @@ __global__ __launch_bounds__(256) void ctcx_traceback(TraceParams tp) {
     } else {
       int kind = tp.top_kind[bp];
       for (int t = sl - 1; t >= 0 && kind >= 0; --t) {
-        const Rec r = rb[(int64_t)t * tp.W + k];
-        out[len++] = kind == 0 ? tp.blank_label : rec_label(r);
-        const uint32_t q = kind == 0 ? rec_bp_blank(r) : rec_bp_nblank(r);
+        uint32_t link, bpb, bpn;
+        int lab;
+        rd(t, link, lab, bpb, bpn);
+        out[len++] = kind == 0 ? tp.blank_label : lab;
+        const uint32_t q = kind == 0 ? bpb : bpn;
         if (q >= kBpRestart) break;
         k = (int)(q >> 1);
         kind = (int)(q & 1u);
@@ -3490,7 +3526,7 @@ hipError_t launch_decode(const DecodeParams<T>& p, hipStream_t s) {
     if (p.W <= 256) return fits_s(256) ? launch_decode_r<T, 2, 256, SC>(p, s) : launch_decode_r<T, 2, 0, SC>(p, s);
     return launch_decode_r<T, 4, 0, SC>(p, s);
   }
-  auto fits = [&](int wc) { return decode_lds_bytes(wc, p.C, (int)sizeof(T)) <= kLdsBytes; };
+  auto fits = [&](int wc) { return decode_lds_bytes(wc, p.C, (int)sizeof(T), false) <= kLdsBytes; };
   if (p.W <= 128) return fits(128) ? launch_decode_r<T, 1, 128>(p, s) : launch_decode_r<T, 1, 0>(p, s);
   if (p.W <= 256) return fits(256) ? launch_decode_r<T, 2, 256>(p, s) : launch_decode_r<T, 2, 0>(p, s);
   return launch_decode_r<T, 4, 0>(p, s);
@@ -3553,3 +3589,35 @@ hipError_t launch_pack(const PackParams& pp, hipStream_t s) {
 #endif  // CTCX_PART == 0
 
 }  // namespace ctcx
+
+#ifdef CTCX_GSTATE
+// ---------------------------------------------------------------------------
+// The global-state tier (this file compiled once more with CTCX_GSTATE, the
+// generic address space for the state and namespace ctcx_gs; csrc/Makefile):
+// shapes whose beam state or row does not fit the LDS (beam_width above the
+// LDS-resident limit, num_classes above the 8-byte record's 65535 or the
+// LDS row) decode with the state in global memory, 16-byte records and the
+// literal path for every frame -- the reference's own algorithm, one lane.
+namespace ctcx {
+template <typename T, class SC>
+static hipError_t launch_decode_gs_t(const DecodeParams<T>& p, hipStream_t s) {
+  hipLaunchKernelGGL((ctcx_beam_decode<T, 1, 0, false, SC>), dim3((unsigned)p.B), dim3(64), 0, s, p);
+  return hipGetLastError();
+}
+}  // namespace ctcx
+
+// Called by the C-ABI layer with its DecodeParams<T> (the same header, so the
+// same layout, in namespace ctcx there).
+hipError_t ctcx_gstate_launch_decode(const void* p, int is_f64, int scored, hipStream_t s) {
+  if (is_f64) {
+    const auto& q = *(const ctcx::DecodeParams<double>*)p;
+    if (q.B == 0) return hipSuccess;
+    return scored ? ctcx::launch_decode_gs_t<double, ctcx::BigramBeamScorer<double>>(q, s)
+                  : ctcx::launch_decode_gs_t<double, ctcx::BaseBeamScorer<double>>(q, s);
+  }
+  const auto& q = *(const ctcx::DecodeParams<float>*)p;
+  if (q.B == 0) return hipSuccess;
+  return scored ? ctcx::launch_decode_gs_t<float, ctcx::BigramBeamScorer<float>>(q, s)
+                : ctcx::launch_decode_gs_t<float, ctcx::BaseBeamScorer<float>>(q, s);
+}
+#endif

@@ -47,6 +47,16 @@ __host__ __device__ inline int rec_label(Rec r) { return (int)((r >> 11) & 0xFFF
 __host__ __device__ inline uint32_t rec_bp_blank(Rec r) { return rec_unbp12((r >> 27) & 0xFFFu); }
 __host__ __device__ inline uint32_t rec_bp_nblank(Rec r) { return rec_unbp12((r >> 39) & 0xFFFu); }
 constexpr int kMaxRecClasses = 65535;
+constexpr int kMaxRecBeam = 512;
+
+// The wide record of the global-state tier (any beam width and num_classes):
+// the same four fields at full width, 16 bytes.
+struct Rec16 {
+  uint32_t link;    // (src branch << 1) | is_new_child
+  int32_t label;    // the beam's last label (-1 at the root)
+  uint32_t bpb;     // best blank-ending alignment back-pointer (pos << 1 | kind), kBpRestart / kBpNone
+  uint32_t bpn;     // best label-ending one
+};
 
 // Per-item results of the decode kernel.
 struct ItemOut {
@@ -103,6 +113,11 @@ struct DecodeParams {
   uint64_t* prof;           // optional [B][8] phase cycle counters (diagnostics)
   const T* scorer_tab;      // bigram beam-scorer table [C + 1][C], or null (BaseBeamScorer)
   const char* prep;         // C > 64: [Tmax][B] row records of ctcx_row_prep (prep_row_bytes each)
+  // global-state tier (ctcx_gs::ctcx_beam_decode): the beam state of item b
+  // at gstate + b * gstate_stride (global memory instead of LDS), records
+  // written as Rec16 through rec
+  char* gstate;
+  int64_t gstate_stride;
 };
 
 struct TraceParams {
@@ -113,6 +128,7 @@ struct TraceParams {
   const int32_t* top_kind;
   int64_t Tmax, B;
   int32_t W, P, merge, blank_label;
+  int32_t rec_wide;   // records are Rec16 (global-state tier), else Rec
   int32_t* seq;    // [B][P][2][Tmax]  walk output, reversed
   int32_t* len;    // [P][2][len_stride], this batch's items at [.][.][0, B)
   int64_t len_stride;
@@ -135,6 +151,14 @@ __host__ __device__ inline int htab_size(int W) {
   return n;
 }
 
+// Bytes of one item's beam state in the global-state tier: the carve without
+// the logit row and the large-C arrays (the row is read in place from the
+// inputs; only the literal path runs there).
+__host__ __device__ inline size_t decode_lds_bytes(int W, int64_t C, int tsize, bool scored);
+__host__ __device__ inline size_t gstate_bytes(int W, int tsize, bool scored) {
+  return (decode_lds_bytes(W, 1, tsize, scored) + 255) & ~(size_t)255;
+}
+
 // LDS bytes needed by the decode kernel (host + device agree on the carve).
 constexpr size_t kLdsBytes = 160 * 1024;   // LDS per CU on gfx950 (one workgroup per item)
 
@@ -145,7 +169,7 @@ __host__ __device__ inline bool decode_inplace(int64_t C) { return C > 64; }
 
 // Bytes of the decode kernel's LDS layout for a beam capacity W (carve() in
 // ctcx_decode.hip, same order and alignment).
-__host__ __device__ inline size_t decode_lds_bytes(int W, int64_t C, int tsize, bool scored = false) {
+__host__ __device__ inline size_t decode_lds_bytes(int W, int64_t C, int tsize, bool scored) {
   const size_t ENC = 3 * (size_t)W + 2;
   const size_t nbuf = decode_inplace(C) ? 1 : 2;
   auto a16 = [](size_t v) { return (v + 15) & ~(size_t)15; };

@@ -22,6 +22,7 @@ CTCEXT_F64 = 1
 CTCEXT_FLAG_FORCE_LITERAL = 1
 CTCEXT_FLAG_PROFILE = 2
 CTCEXT_FLAG_PHASES = 4
+CTCEXT_FLAG_GLOBAL_STATE = 8   # testing: the global-state tier whatever the shape
 CTCEXT_SCORER_BASE = 0
 CTCEXT_SCORER_BIGRAM = 1
 
@@ -67,7 +68,7 @@ class Stats(ctypes.Structure):
                 ("no_label_paths", ctypes.c_int64),
                 ("decode_kernel_ms", ctypes.c_double), ("norm_kernel_ms", ctypes.c_double),
                 ("traceback_ms", ctypes.c_double), ("n_devices", ctypes.c_int32),
-                ("pad_", ctypes.c_int32)]
+                ("tier", ctypes.c_int32)]
 
 
 _lib = None

@@ -107,7 +107,7 @@ class Decoder:
     def stats(self):
         s = _lib.Stats()
         self.lib.ctcext_get_stats(self.handle, ctypes.byref(s))
-        return {k: getattr(s, k) for k, _ in _lib.Stats._fields_ if k != "pad_"}
+        return {k: getattr(s, k) for k, _ in _lib.Stats._fields_}
 
     # -- phase 1 ---------------------------------------------------------
     def decode(self, args):

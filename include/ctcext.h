@@ -50,7 +50,8 @@ enum { CTCEXT_SCORER_BASE = 0, CTCEXT_SCORER_BIGRAM = 1 };
 enum {
   CTCEXT_FLAG_FORCE_LITERAL = 1,   /* testing: replay every frame through the literal TopN model */
   CTCEXT_FLAG_PROFILE = 2,         /* time the decode kernel with HIP events (ctcext_stats) */
-  CTCEXT_FLAG_PHASES = 4           /* diagnostics: per-item s_memtime phase counters */
+  CTCEXT_FLAG_PHASES = 4,          /* diagnostics: per-item s_memtime phase counters */
+  CTCEXT_FLAG_GLOBAL_STATE = 8     /* testing: decode on the global-state tier whatever the shape */
 };
 
 typedef struct ctcext_decoder ctcext_decoder;
@@ -115,7 +116,8 @@ typedef struct {
   double norm_kernel_ms;
   double traceback_ms;             /* traceback + scan */
   int32_t n_devices;               /* devices of the handle */
-  int32_t pad_;
+  int32_t tier;                    /* last decode: 0 the LDS-resident fast tier, 1 the
+                                      global-state tier (shapes past the LDS / record limits) */
 } ctcext_stats;
 
 /* Handle lifetime.  A handle owns a HIP stream and a grow-only device
@@ -162,8 +164,11 @@ int ctcext_phase_counters(ctcext_decoder* dec, uint64_t* out, int64_t n);
 /* Message of the last failing call on this thread ("" if none). */
 const char* ctcext_last_error(void);
 
-/* Maximum beam width supported on this device for the given class count and
- * dtype (the per-item beam state is LDS-resident). */
+/* Widest beam the LDS-resident fast tier decodes for the given class count
+ * and dtype (0: num_classes is past that tier).  Wider beams, and num_classes
+ * above 65535 or the LDS row, decode on the global-state tier (beam state in
+ * HBM, 16-byte records, the literal path every frame): any shape the
+ * reference accepts, at a lower rate. */
 int32_t ctcext_max_beam_width(int64_t num_classes, int32_t dtype);
 
 #ifdef __cplusplus

@@ -46,6 +46,17 @@ def test_library_exports_every_declared_symbol():
         assert ctypes.cast(getattr(lib, name), ctypes.c_void_p).value
 
 
+def test_every_shape_validates():
+    # no shape limit of its own below the 32-bit indices: num_classes above the
+    # 8-byte record (65535) and beams past the LDS tier validate (they decode
+    # on the global-state tier)
+    lib = _lib.load()
+    for shape, W in (((3, 1, 70000), 8), ((3, 1, 29), 2048), ((3, 1, 200000), 600)):
+        a, keep = _args(shape, [3], W=W)
+        assert lib.ctcext_validate(ctypes.byref(a)) == _lib.CTCEXT_OK, lib.ctcext_last_error()
+    assert lib.ctcext_max_beam_width(70000, _lib.CTCEXT_F32) == 0   # past the fast tier
+
+
 def test_max_beam_width_is_host_only_and_monotone():
     lib = _lib.load()
     w29 = lib.ctcext_max_beam_width(29, _lib.CTCEXT_F32)
@@ -118,8 +129,8 @@ def _args(shape, sl, dims=None, sl_dims=1, sl_size=None, W=4, P=1, blank=0, dtyp
      "requested more paths than the beam width."),
     (dict(shape=(3, 1, 4), sl=[3], blank=4), _lib.CTCEXT_INVALID_ARGUMENT,
      "blank_index out of range [0, num_classes)"),
-    (dict(shape=(3, 1, 70000), sl=[3]), _lib.CTCEXT_UNIMPLEMENTED,
-     "num_classes 70000 exceeds the back-pointer record format (max 65535)"),
+    (dict(shape=(3, 1, 1 << 30), sl=[3]), _lib.CTCEXT_UNIMPLEMENTED,
+     "num_classes or beam_width beyond this library's 32-bit indices"),
     (dict(shape=(3, 1, 4), sl=[3], dtype=7), _lib.CTCEXT_INVALID_ARGUMENT, "dtype must be float32 or float64"),
 ])
 def test_c_abi_validation(kw, code, msg):

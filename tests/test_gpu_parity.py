@@ -50,12 +50,12 @@ def test_paper_golden_f32(device):
     compare(out, ref, a["top_paths"])
 
 
-def _run_random(seed, n, **kw_case):
+def _run_random(seed, n, flags=0, device=False, **kw_case):
     rng = np.random.default_rng(seed)
     for it in range(n):
         x, sl, W, P, kw = random_case(rng, **kw_case)
         ref, rerr = oracle_or_error(x, sl, W, P, kw)
-        out, gerr = _gpu_or_error(x, sl, W, P, kw)
+        out, gerr = _gpu_or_error(x, sl, W, P, kw, flags=flags, device=device and it % 2 == 1)
         assert rerr == gerr, (it, rerr, gerr)
         if ref is not None:
             compare(out, ref, P)
@@ -464,6 +464,59 @@ def test_full_length_golden(name):
     compare(out, oracle.OracleOutput(di, dv, ds, ai, av, ash, lp), P)
 
 
+# ---- the global-state tier: beam state in HBM, 16-byte records, the literal
+# path every frame (ctcx_decode.hip CTCX_GSTATE) -- the shapes the LDS tier
+# cannot hold (num_classes > 65535 or past the LDS row, beams past the
+# LDS-resident state), forced onto every random family by a testing flag
+
+GS = _lib.CTCEXT_FLAG_GLOBAL_STATE
+
+
+def _tier():
+    return ctcext_amd.get_decoder(0).last_stats["tier"]
+
+
+def test_global_state_tier_random_families():
+    _run_random(7001, 60, flags=GS, device=True)
+    assert _tier() == 1
+    _run_random(7002, 40, flags=GS, ties=True)
+    _run_random(7003, 15, flags=GS, T_max=30, B_max=2, C_min=65, C_max=300, W_max=100)
+    _run_random(7004, 30, flags=GS, dtype=np.float64)
+    _run_random(7005, 40, flags=GS, neg_inf=True)
+
+
+def test_global_state_tier_duplicate_entries():
+    for k, (x, sl, W, P, kw, ref, nd) in enumerate(_dup_family(31337, 15)):
+        out, err = _gpu_or_error(x, sl, W, P, kw, flags=GS)
+        assert err is None, (k, err)
+        compare(out, ref, P)
+        assert _dup_frames() == nd, (k, _dup_frames(), nd)
+
+
+@pytest.mark.parametrize("T,B,C,W,P,merge,blank", [
+    (12, 2, 70000, 8, 2, True, 0),        # num_classes past the 8-byte record (65535)
+    (6, 1, 131072, 4, 1, False, 131071),  # ... and past any LDS row; blank last
+    (40, 2, 8, 600, 3, True, 0),          # beams past the LDS-resident state
+    (25, 2, 5, 1000, 2, False, 2),        # ... and past 512 (the 8-byte record's link)
+])
+def test_global_state_tier_shapes(T, B, C, W, P, merge, blank):
+    rng = np.random.default_rng(T * 7 + C)
+    x = rng.standard_normal((T, B, C)).astype(np.float32)
+    sl = np.array([T, max(T - 3, 1)][:B], np.int32)
+    kw = dict(merge_repeated=merge, blank_index=blank, blank_label=-1)
+    ref = oracle.decode(x, sl, W, P, **kw)
+    out, err = _gpu_or_error(x, sl, W, P, kw, device=True)
+    assert err is None, err
+    assert _tier() == 1
+    compare(out, ref, P)
+
+
+def test_lds_tier_is_used_within_its_limits():
+    x = np.random.default_rng(1).standard_normal((10, 2, 29)).astype(np.float32)
+    out, err = _gpu_or_error(x, np.array([10, 8], np.int32), 128, 2, dict(merge_repeated=True))
+    assert err is None and _tier() == 0
+
+
 # ---- beam-scorer hook (util/ctc_beam_scorer.h:31-65).  Parity unpinned: the
 # reference op always runs BaseBeamScorer (kernels.cc:260), so the bigram
 # scorer's only checker is the oracle's restatement of the hook call sites
@@ -516,6 +569,11 @@ def test_scorer_large_c_and_neg_inf():
     # large C runs the skip scans, whose bounds need scores <= 0
     _run_scored(6006, 12, T_max=30, B_max=2, C_min=65, C_max=300, W_max=100, scale=4.0)
     _run_scored(6007, 30, neg_inf=True)
+
+
+def test_scorer_global_state_tier():
+    _run_scored(6009, 30, flags=GS)
+    _run_scored(6010, 10, dtype=np.float64, flags=GS)
 
 
 def test_scorer_zero_table_is_identity():
