@@ -2960,6 +2960,9 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     // frame-start arrays (by source position) is taken into registers before
     // the first write (by sorted position); KM positions per lane.
     constexpr bool INPLACE = BIG;
+    // staged (unrolled, KM positions per lane) for a compile-time capacity, and
+    // always in place (the LDS tier: W <= 512); plain loops otherwise (any W)
+    constexpr bool STAGED = WC > 0 || INPLACE;
     constexpr int KM = (WC > 0 ? WC : 512) / 64;
     const int nx = INPLACE ? buf : buf ^ 1;
     for (int i = lane; i < nb; i += 64) cx.newpos[i] = -1;
@@ -3042,14 +3045,16 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
       prm.rec[((int64_t)b * prm.Tmax + t) * W + k] = rec_pack(kd, cx.elab[e], bpb, bpn);
 #endif
     };
-    if constexpr (INPLACE) {
+    if constexpr (STAGED) {
+      // KM positions per lane, unrolled, so each phase's chains of dependent
+      // LDS reads overlap across positions
       uint64_t nha[KM], nhb[KM];
 #pragma unroll
       for (int j = 0; j < KM; ++j) {
         nha[j] = nhb[j] = 0;
         if (lane + 64 * j < n) hash_of(lane + 64 * j, nha[j], nhb[j]);
       }
-      __syncthreads();
+      if constexpr (INPLACE) __syncthreads();
 #pragma unroll
       for (int j = 0; j < KM; ++j)
         if (lane + 64 * j < n) put_hash(lane + 64 * j, nha[j], nhb[j]);
@@ -3061,7 +3066,7 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
         nfl[j] = 0;
         if (lane + 64 * j < n) parent_of(lane + 64 * j, npar[j], nfl[j]);
       }
-      __syncthreads();
+      if constexpr (INPLACE) __syncthreads();
 #pragma unroll
       for (int j = 0; j < KM; ++j)
         if (lane + 64 * j < n) put_branch(lane + 64 * j, npar[j], nfl[j]);
