@@ -27,7 +27,7 @@ hipError_t launch_row_norm(const T* x, const int32_t* sl, T* norm, int64_t T_, i
                            int64_t xstride, hipStream_t s);
 hipError_t launch_traceback(const TraceParams& tp, hipStream_t s);
 template <typename T>
-hipError_t launch_row_prep(const T* x, const int32_t* sl, char* prep, int64_t T_, int64_t B, int64_t C,
+hipError_t launch_row_prep(const T* x, const int32_t* sl, char* prep, T* norm, int64_t T_, int64_t B, int64_t C,
                            int64_t xstride, int blank, hipStream_t s);
 hipError_t launch_scan(const int32_t* len, int64_t* off, int64_t* res, int64_t B, int P, hipStream_t s);
 hipError_t launch_pack(const PackParams& pp, hipStream_t s);
@@ -377,9 +377,14 @@ static int enqueue_shard(ctcext_decoder* d, Dev& v, bool root, const ctcext_deco
   }
 
   if (prof) HIP_OR_FAIL(hipEventRecord(v.ev[0], s));
-  HIP_OR_FAIL(ctcx::launch_row_norm<T>(x, sl, (T*)v.norm.p, T_, Bs, C, xstride, s));
-  // large C: the row facts the decode kernel reads per frame (parallel pre-pass)
-  if (!gs) HIP_OR_FAIL(ctcx::launch_row_prep<T>(x, sl, (char*)v.prep.p, T_, Bs, C, xstride, a->blank_index, s));
+  if (!gs && C > 64) {
+    // large C: the normaliser and the row facts the decode kernel reads per
+    // frame, one parallel pre-pass
+    HIP_OR_FAIL(ctcx::launch_row_prep<T>(x, sl, (char*)v.prep.p, (T*)v.norm.p, T_, Bs, C, xstride,
+                                         a->blank_index, s));
+  } else {
+    HIP_OR_FAIL(ctcx::launch_row_norm<T>(x, sl, (T*)v.norm.p, T_, Bs, C, xstride, s));
+  }
   if (prof) HIP_OR_FAIL(hipEventRecord(v.ev[1], s));
 
   ctcx::DecodeParams<T> p{};

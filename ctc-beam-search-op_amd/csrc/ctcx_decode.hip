@@ -3204,55 +3204,95 @@ __global__ __launch_bounds__(64) void ctcx_row_norm(const T* __restrict__ x, con
 
 #if CTCX_PART == 0
 // ---------------------------------------------------------------------------
-// Large C (> 64): the row facts the decode kernel needs per frame (RowHdr,
-// block maxima, top set S; ctcx_kernels.h), for every (t, b) row, one wave
-// per row.  Fully parallel over rows: inside the decode kernel the same work
-// sat on the one-wave T-serial chain (at C=5000 the top-set bisection alone
-// took ~108k cycles per frame there).
-//   * block maxima: 64 classes per step, one wave max each, in class order;
-//   * S: bisection on the order-preserving integer key of the float for the
-//     smallest tau with |{non-blank x : key >= tau}| <= kTopK; any bracket
-//     keeping cnt(lo) > kTopK >= cnt(hi) yields the same S (the row's kTopK
-//     largest values without a tie across the boundary); the keys are staged
-//     in LDS when the row fits (kPrepLdsClasses), else re-read from global
-//     memory.
-// Rows past an item's length are skipped (never read).
-constexpr int kPrepLdsClasses = 16384;
+// Large C (> 64): everything the decode kernel needs per row that depends on
+// the row alone, one wave per (t, b) row, fully parallel over rows (inside
+// the decode kernel the same work sat on the one-wave T-serial chain; at
+// C=5000 the top-set bisection alone took ~108k cycles per frame there):
+//   * the softmax normaliser (decoder.h:72-80; replaces ctcx_row_norm for
+//     these rows): the exp terms in parallel, then one lane sums them in class
+//     order, as the reference does;
+//   * RowHdr: the row maximum, the NaN / +inf test, |S| and the largest value
+//     outside S;
+//   * the 64-class block maxima;
+//   * S (float rows): bisection on the order-preserving integer key of the
+//     float for the smallest tau with |{non-blank x : key >= tau}| <= K =
+//     kTopK; any bracket keeping cnt(lo) > K >= cnt(hi) yields the
+//     same S (the row's K largest values without a tie across the boundary).
+// The row is staged in LDS (batches of loads in flight) when it fits
+// (kPrepLdsBytes); wider rows are read from global memory.  Rows past an
+// item's length are skipped (never read).
+constexpr size_t kPrepLdsBytes = 128 * 1024;
+constexpr int kPrepBatch = 16;     // loads in flight per lane while staging
+constexpr int kPrepCompact = 256;  // keys at or above the bracket's lower end, bisected in registers
 
 __device__ __forceinline__ unsigned fkey(float v) {
   const unsigned u = __float_as_uint(v);
   return u ^ ((u >> 31) ? 0xFFFFFFFFu : 0x80000000u);
 }
 
-template <typename T>
+template <typename T, bool INLDS>
 __global__ __launch_bounds__(64) void ctcx_row_prep(const T* __restrict__ x, const int32_t* __restrict__ seq_len,
-                                                   char* __restrict__ prep, int64_t B, int64_t C, int64_t xstride,
-                                                   int blank) {
-  extern __shared__ __attribute__((aligned(16))) unsigned pkeys[];   // float rows: keys by class
+                                                   char* __restrict__ prep, T* __restrict__ norm, int64_t B,
+                                                   int64_t C, int64_t xstride, int blank) {
+  extern __shared__ __attribute__((aligned(16))) char plds[];
+  T* xs = (T*)plds;   // the staged row
   const int lane = threadIdx.x;
   const int64_t row = blockIdx.x;
   const int64_t t = row / B, b = row - t * B;
   if (t >= seq_len[b]) return;
   const T NI = ninf<T>();
+  const int Ci = (int)C;
   const T* xr = x + (t * xstride + b) * C;
   char* pr = prep + row * (int64_t)prep_row_bytes(C, (int)sizeof(T));
   T* bm = (T*)(pr + prep_bmax_offset((int)sizeof(T)));
-  const int nblk = (int)((C + 63) / 64);
-  const bool inlds = sizeof(T) == 4 && C <= kPrepLdsClasses;
-  T xmax = NI, bmv = NI;
-  bool bad = false;
-  for (int k = 0; k < nblk; ++k) {
-    const int j = k * 64 + lane;
-    const T xv = j < C ? xr[j] : NI;
-    bad |= (xv != xv) || (xv == pinf<T>());
-    xmax = xv > xmax ? xv : xmax;
-    const T m = wave_max(xv);
-    bmv = (lane == (k & 63)) ? m : bmv;
-    if ((k & 63) == 63 || k == nblk - 1) {
-      if (lane <= (k & 63)) bm[(k & ~63) + lane] = bmv;
+  const int nblk = (Ci + 63) / 64;
+  constexpr bool inlds = INLDS;   // the launcher's choice: C * sizeof(T) <= kPrepLdsBytes
+  if (inlds) {
+    for (int j0 = 0; j0 < Ci; j0 += 64 * kPrepBatch) {
+      T v[kPrepBatch];
+#pragma unroll
+      for (int u = 0; u < kPrepBatch; ++u) {
+        const int j = j0 + 64 * u + lane;
+        v[u] = j < Ci ? xr[j] : T(0);
+      }
+#pragma unroll
+      for (int u = 0; u < kPrepBatch; ++u) {
+        const int j = j0 + 64 * u + lane;
+        if (j < Ci) xs[j] = v[u];
+      }
     }
-    if constexpr (sizeof(T) == 4) {
-      if (inlds && j < C) pkeys[j] = fkey((float)xv);
+    __syncthreads();
+  }
+  auto xat = [&](int j) -> T { return inlds ? xs[j] : xr[j]; };
+  // maximum, NaN / +inf, block maxima (block k: classes [64k, 64k + 64)),
+  // and (float) the lane's largest non-blank key
+  T xmax = NI, bmv = NI;
+  bool bad = false, nan = false;
+  unsigned lkmax = 0u;
+  for (int k0 = 0; k0 < nblk; k0 += 8) {
+    T v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = (k0 + u) * 64 + lane;
+      v[u] = (k0 + u < nblk && j < Ci) ? xat(j) : NI;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = k0 + u;
+      if (k >= nblk) break;
+      nan |= v[u] != v[u];
+      bad |= (v[u] != v[u]) || (v[u] == pinf<T>());
+      xmax = v[u] > xmax ? v[u] : xmax;
+      if constexpr (sizeof(T) == 4) {
+        const int j = k * 64 + lane;
+        const unsigned kv = fkey((float)v[u]);
+        if (j < Ci && j != blank && kv > lkmax) lkmax = kv;
+      }
+      const T m = wave_max(v[u]);
+      bmv = (lane == (k & 63)) ? m : bmv;
+      if ((k & 63) == 63 || k == nblk - 1) {
+        if (lane <= (k & 63)) bm[(k & ~63) + lane] = bmv;
+      }
     }
   }
   RowHdr<T> h;
@@ -3261,25 +3301,76 @@ __global__ __launch_bounds__(64) void ctcx_row_prep(const T* __restrict__ x, con
   h.ns = 0;
   h.xout = pinf<T>();
   if constexpr (sizeof(T) == 4) {
-    const int Cm1 = (int)C - 1;
-    auto kat = [&](int j) -> unsigned { return inlds ? pkeys[j] : fkey(xr[j]); };
+    const int Cm1 = Ci - 1;
+    const int K = kTopK;
     // |{non-blank labels with key >= tau}|: per-lane counts, then one wave sum
     auto cnt_ge = [&](unsigned tau) {
       int c = 0;
-      for (int j = lane; j < (int)C; j += 64) c += (j != blank && kat(j) >= tau) ? 1 : 0;
+      int j = lane;
+      for (; j + 64 * 7 < Ci; j += 64 * 8) {   // 8 reads in flight
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = xat(j + 64 * u);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) c += (j + 64 * u != blank && fkey(v[u]) >= tau) ? 1 : 0;
+      }
+      for (; j < Ci; j += 64) c += (j != blank && fkey(xat(j)) >= tau) ? 1 : 0;
 #pragma unroll
       for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o);
       return uni(c);
     };
     uint64_t lo = 0, hi = 0;
-    if (Cm1 > kTopK) {
-      hi = (uint64_t)fkey((float)h.xmax) + 1ull;   // cnt(hi) = 0; cnt(lo = 0) = Cm1 > kTopK
-      while (hi - lo > 1) {
-        const uint64_t mid = (lo + hi) >> 1;
-        const int c = cnt_ge((unsigned)mid);
-        if (c <= kTopK) hi = mid;
-        else lo = mid;
-        if (c == kTopK) break;
+    if (Cm1 > K) {
+      static_assert(kTopK == 64, "the bracket below takes one key per lane");
+      hi = (uint64_t)fkey(h.xmax) + 1ull;   // cnt(hi) = 0
+      // the smallest lane maximum km has at least 64 keys at or above it (one
+      // per lane: each lane's largest); Cm1 > 64 gives every lane a label
+      const unsigned km = (unsigned)uni((int)wave_min(lkmax));
+      const int ckm = cnt_ge(km);
+      if (ckm == K) {
+        lo = km - 1;   // exactly the K largest: tau = km
+        hi = km;
+      } else {
+        lo = km;       // cnt(km) > K
+        CTCX_LDS unsigned* cks = (CTCX_LDS unsigned*)(plds + (INLDS ? ((size_t)C * sizeof(T) + 15) & ~(size_t)15 : 0));
+        if (ckm <= kPrepCompact) {
+          // every key >= km into a compact list (at most kPrepCompact), then
+          // bisect in registers: tau > km, so S lies in the list
+          int n = 0;
+          for (int j0 = 0; j0 < Ci; j0 += 64) {
+            const int j = j0 + lane;
+            const unsigned kv = j < Ci ? fkey(xat(j)) : 0u;
+            const bool in = j < Ci && j != blank && kv >= km;
+            const uint64_t m = __ballot(in);
+            if (in) cks[n + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u))] = kv;
+            n += __builtin_popcountll(m);
+          }
+          __syncthreads();
+          unsigned ck[kPrepCompact / 64];
+#pragma unroll
+          for (int q = 0; q < kPrepCompact / 64; ++q) ck[q] = 64 * q + lane < n ? cks[64 * q + lane] : 0u;
+          while (hi - lo > 1) {
+            const uint64_t mid = (lo + hi) >> 1;
+            int c = 0;
+#pragma unroll
+            for (int q = 0; q < kPrepCompact / 64; ++q) c += ck[q] >= (unsigned)mid ? 1 : 0;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o);
+            c = uni(c);
+            if (c <= K) hi = mid;
+            else lo = mid;
+            if (c == K) break;
+          }
+        } else {
+          while (hi - lo > 1) {
+            const uint64_t mid = (lo + hi) >> 1;
+            const int c = cnt_ge((unsigned)mid);
+            if (c <= K) hi = mid;
+            else lo = mid;
+            if (c == K) break;
+          }
+        }
       }
     }
     const unsigned tau = (unsigned)hi;
@@ -3291,8 +3382,7 @@ __global__ __launch_bounds__(64) void ctcx_row_prep(const T* __restrict__ x, con
       bool in = false;
       float v = 0.f;
       if (xi < Cm1) {
-        const int j = xi + (xi >= blank ? 1 : 0);
-        v = (float)xr[j];
+        v = xat(xi + (xi >= blank ? 1 : 0));
         in = fkey(v) >= tau;
         if (!in) xo = v > xo ? v : xo;
       }
@@ -3304,9 +3394,40 @@ __global__ __launch_bounds__(64) void ctcx_row_prep(const T* __restrict__ x, con
       n += __builtin_popcountll(m);
     }
     h.ns = n;
-    h.xout = (T)wave_max(xo);
+    h.xout = wave_max(xo);
   }
   if (lane == 0) *(RowHdr<T>*)pr = h;
+  // the normaliser: m = the row maximum -- in class order when a NaN is
+  // present (max is order-free otherwise), as ctcx_row_norm and the reference
+  // take it -- then s = sum of exp(x_j - m) in class order, norm = m + log(s)
+  T m = h.xmax;
+  if (__ballot(nan) != 0ull) {
+    m = xat(0);
+    for (int j = 1; j < Ci; ++j) {
+      const T v = xat(j);
+      m = (v > m) ? v : m;
+    }
+  }
+  T ssum = T(0);
+  if (inlds) {
+    __syncthreads();
+    for (int j = lane; j < Ci; j += 64) xs[j] = norm_exp(xs[j] - m);
+    __syncthreads();
+    if (lane == 0) {
+      int j = 0;
+      for (; j + 16 <= Ci; j += 16) {
+        T e[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) e[u] = xs[j + u];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) ssum += e[u];
+      }
+      for (; j < Ci; ++j) ssum += xs[j];
+    }
+  } else if (lane == 0) {
+    for (int j = 0; j < Ci; ++j) ssum += norm_exp(xr[j] - m);
+  }
+  if (lane == 0) norm[row] = m + norm_log(ssum);
 }
 
 // ---------------------------------------------------------------------------
@@ -3541,23 +3662,30 @@ template hipError_t launch_decode<float>(const DecodeParams<float>&, hipStream_t
 template hipError_t launch_decode<double>(const DecodeParams<double>&, hipStream_t);
 
 template <typename T>
-hipError_t launch_row_prep(const T* x, const int32_t* sl, char* prep, int64_t T_, int64_t B, int64_t C,
+hipError_t launch_row_prep(const T* x, const int32_t* sl, char* prep, T* norm, int64_t T_, int64_t B, int64_t C,
                            int64_t xstride, int blank, hipStream_t s) {
   const int64_t rows = T_ * B;
   if (rows == 0 || C <= 64) return hipSuccess;
-  const size_t lds = (sizeof(T) == 4 && C <= kPrepLdsClasses) ? (size_t)C * 4 : 0;
+  const size_t row_b = (size_t)C * sizeof(T);
+  const size_t lds = ((row_b + 15) & ~(size_t)15) + 4 * kPrepCompact;   // the row, then the compact key list
+  if (row_b > kPrepLdsBytes) {   // the row is read from global memory
+    hipLaunchKernelGGL((ctcx_row_prep<T, false>), dim3((unsigned)rows), dim3(64), 4 * kPrepCompact, s, x, sl, prep,
+                       norm, B, C, xstride, blank);
+    return hipGetLastError();
+  }
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)ctcx_row_prep<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)lds);
+    hipError_t e = hipFuncSetAttribute((const void*)ctcx_row_prep<T, true>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(ctcx_row_prep<T>, dim3((unsigned)rows), dim3(64), lds, s, x, sl, prep, B, C, xstride, blank);
+  hipLaunchKernelGGL((ctcx_row_prep<T, true>), dim3((unsigned)rows), dim3(64), lds, s, x, sl, prep, norm, B, C,
+                     xstride, blank);
   return hipGetLastError();
 }
-template hipError_t launch_row_prep<float>(const float*, const int32_t*, char*, int64_t, int64_t, int64_t, int64_t,
-                                           int, hipStream_t);
-template hipError_t launch_row_prep<double>(const double*, const int32_t*, char*, int64_t, int64_t, int64_t, int64_t,
-                                            int, hipStream_t);
+template hipError_t launch_row_prep<float>(const float*, const int32_t*, char*, float*, int64_t, int64_t, int64_t,
+                                           int64_t, int, hipStream_t);
+template hipError_t launch_row_prep<double>(const double*, const int32_t*, char*, double*, int64_t, int64_t,
+                                            int64_t, int64_t, int, hipStream_t);
 
 template <typename T>
 hipError_t launch_row_norm(const T* x, const int32_t* sl, T* norm, int64_t T_, int64_t B, int64_t C,

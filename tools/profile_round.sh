@@ -16,11 +16,11 @@ export TMPDIR=/tmp
 cd /tmp
 step() { echo "[$(date +%T)] $*" >> $O/steps.log; }
 step stats-cfg3
-timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats_cfg3 -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu --no-host-io > $O/stats_cfg3.log 2>&1 || exit 11
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats_cfg3 -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu --no-host-io --no-strong > $O/stats_cfg3.log 2>&1 || exit 11
 step fetch-cfg3
-timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch_cfg3 -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu --no-host-io > $O/fetch_cfg3.log 2>&1 || exit 12
+timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch_cfg3 -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu --no-host-io --no-strong > $O/fetch_cfg3.log 2>&1 || exit 12
 step write-cfg3
-timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write_cfg3 -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu --no-host-io > $O/write_cfg3.log 2>&1 || exit 13
+timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write_cfg3 -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu --no-host-io --no-strong > $O/write_cfg3.log 2>&1 || exit 13
 step fetch-calib
 timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch_calib -o run -- $R/tools/fetch_calib > $O/calib.json 2> $O/fetch_calib.log || exit 14
 step write-calib
@@ -34,8 +34,8 @@ timeout -k 10 300 python3 bench.py > $O/bench_cfg3.json 2> $O/bench_cfg3.err || 
 if [ "$QUICK" != 1 ]; then
   cd /tmp
   step stats-cfg4
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats_cfg4 -o run -- python3 $R/bench.py --config cfg4 --steps 2 --warmup 1 --no-cpu --no-host-io > $O/stats_cfg4.log 2>&1 || exit 18
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats_cfg4 -o run -- python3 $R/bench.py --config cfg4 --steps 2 --warmup 1 --no-cpu --no-host-io --no-strong > $O/stats_cfg4.log 2>&1 || exit 18
   step stats-cfg5
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats_cfg5 -o run -- python3 $R/bench.py --config cfg5 --steps 1 --warmup 1 --no-cpu --no-host-io > $O/stats_cfg5.log 2>&1 || exit 19
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats_cfg5 -o run -- python3 $R/bench.py --config cfg5 --steps 1 --warmup 1 --no-cpu --no-host-io --no-strong > $O/stats_cfg5.log 2>&1 || exit 19
 fi
 step done
