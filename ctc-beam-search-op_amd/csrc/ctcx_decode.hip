@@ -108,6 +108,50 @@ __device__ __forceinline__ T wave_max(T v) {
   return v;
 }
 
+// Wave reductions without LDS traffic (for NaN-free data; the order of the
+// comparisons differs from wave_max's): a prefix max/min/sum inside each row
+// of 16 lanes by DPP row shifts, then the four row results by readlane.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v, float ident) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, ident),
+                                                               __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v, int ident) {
+  return __builtin_amdgcn_update_dpp(ident, v, CTRL, 0xf, 0xf, false);
+}
+__device__ __forceinline__ float wave_max_dpp(float v) {
+  const float I = -__builtin_inff();
+  float w;
+  w = dpp_f<0x111>(v, I); v = w > v ? w : v;   // row_shr:1
+  w = dpp_f<0x112>(v, I); v = w > v ? w : v;   // row_shr:2
+  w = dpp_f<0x114>(v, I); v = w > v ? w : v;   // row_shr:4
+  w = dpp_f<0x118>(v, I); v = w > v ? w : v;   // row_shr:8
+  const float a = bcast(v, 15), b = bcast(v, 31), c = bcast(v, 47), d = bcast(v, 63);
+  const float ab = a > b ? a : b, cd = c > d ? c : d;
+  return ab > cd ? ab : cd;
+}
+__device__ __forceinline__ double wave_max_dpp(double v) { return wave_max(v); }
+__device__ __forceinline__ unsigned wave_min_dpp(unsigned v) {
+  const int I = -1;   // 0xffffffff
+  int x = (int)v, w;
+  w = dpp_i<0x111>(x, I); x = (unsigned)w < (unsigned)x ? w : x;
+  w = dpp_i<0x112>(x, I); x = (unsigned)w < (unsigned)x ? w : x;
+  w = dpp_i<0x114>(x, I); x = (unsigned)w < (unsigned)x ? w : x;
+  w = dpp_i<0x118>(x, I); x = (unsigned)w < (unsigned)x ? w : x;
+  const unsigned a = (unsigned)bcast(x, 15), b = (unsigned)bcast(x, 31), c = (unsigned)bcast(x, 47),
+                 d = (unsigned)bcast(x, 63);
+  const unsigned ab = a < b ? a : b, cd = c < d ? c : d;
+  return ab < cd ? ab : cd;
+}
+__device__ __forceinline__ int wave_sum_dpp(int x) {
+  x += dpp_i<0x111>(x, 0);
+  x += dpp_i<0x112>(x, 0);
+  x += dpp_i<0x114>(x, 0);
+  x += dpp_i<0x118>(x, 0);
+  return bcast(x, 15) + bcast(x, 31) + bcast(x, 47) + bcast(x, 63);
+}
+
 // "first-pushed maximum" of a std::priority_queue with a strict '<' comparer
 // (ctc_beam_entry.h:65-73): only a strictly greater push replaces the top.
 template <typename T>
@@ -3224,6 +3268,7 @@ __global__ __launch_bounds__(64) void ctcx_row_norm(const T* __restrict__ x, con
 constexpr size_t kPrepLdsBytes = 128 * 1024;
 constexpr int kPrepBatch = 16;     // loads in flight per lane while staging
 constexpr int kPrepCompact = 256;  // keys at or above the bracket's lower end, bisected in registers
+constexpr size_t kPrepTabBytes = 256;  // LDS copy of expf's 2^(i/32) table
 
 __device__ __forceinline__ unsigned fkey(float v) {
   const unsigned u = __float_as_uint(v);
@@ -3234,8 +3279,10 @@ template <typename T, bool INLDS>
 __global__ __launch_bounds__(64) void ctcx_row_prep(const T* __restrict__ x, const int32_t* __restrict__ seq_len,
                                                    char* __restrict__ prep, T* __restrict__ norm, int64_t B,
                                                    int64_t C, int64_t xstride, int blank) {
+  // LDS: the expf table (32 x 8 bytes), the staged row, the compact key list
   extern __shared__ __attribute__((aligned(16))) char plds[];
-  T* xs = (T*)plds;   // the staged row
+  uint64_t* etab = (uint64_t*)plds;
+  T* xs = (T*)(plds + kPrepTabBytes);
   const int lane = threadIdx.x;
   const int64_t row = blockIdx.x;
   const int64_t t = row / B, b = row - t * B;
@@ -3247,6 +3294,7 @@ __global__ __launch_bounds__(64) void ctcx_row_prep(const T* __restrict__ x, con
   T* bm = (T*)(pr + prep_bmax_offset((int)sizeof(T)));
   const int nblk = (Ci + 63) / 64;
   constexpr bool inlds = INLDS;   // the launcher's choice: C * sizeof(T) <= kPrepLdsBytes
+  if (lane < 32) etab[lane] = gm::exp2f_tab(lane);   // read after the staging barrier
   if (inlds) {
     for (int j0 = 0; j0 < Ci; j0 += 64 * kPrepBatch) {
       T v[kPrepBatch];
@@ -3288,7 +3336,7 @@ __global__ __launch_bounds__(64) void ctcx_row_prep(const T* __restrict__ x, con
         const unsigned kv = fkey((float)v[u]);
         if (j < Ci && j != blank && kv > lkmax) lkmax = kv;
       }
-      const T m = wave_max(v[u]);
+      const T m = wave_max_dpp(v[u]);
       bmv = (lane == (k & 63)) ? m : bmv;
       if ((k & 63) == 63 || k == nblk - 1) {
         if (lane <= (k & 63)) bm[(k & ~63) + lane] = bmv;
@@ -3296,7 +3344,7 @@ __global__ __launch_bounds__(64) void ctcx_row_prep(const T* __restrict__ x, con
     }
   }
   RowHdr<T> h;
-  h.xmax = wave_max(xmax);
+  h.xmax = wave_max_dpp(xmax);
   h.bad = __ballot(bad) != 0ull;
   h.ns = 0;
   h.xout = pinf<T>();
@@ -3315,9 +3363,7 @@ __global__ __launch_bounds__(64) void ctcx_row_prep(const T* __restrict__ x, con
         for (int u = 0; u < 8; ++u) c += (j + 64 * u != blank && fkey(v[u]) >= tau) ? 1 : 0;
       }
       for (; j < Ci; j += 64) c += (j != blank && fkey(xat(j)) >= tau) ? 1 : 0;
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o);
-      return uni(c);
+      return uni(wave_sum_dpp(c));
     };
     uint64_t lo = 0, hi = 0;
     if (Cm1 > K) {
@@ -3325,14 +3371,15 @@ __global__ __launch_bounds__(64) void ctcx_row_prep(const T* __restrict__ x, con
       hi = (uint64_t)fkey(h.xmax) + 1ull;   // cnt(hi) = 0
       // the smallest lane maximum km has at least 64 keys at or above it (one
       // per lane: each lane's largest); Cm1 > 64 gives every lane a label
-      const unsigned km = (unsigned)uni((int)wave_min(lkmax));
+      const unsigned km = (unsigned)uni((int)wave_min_dpp(lkmax));
       const int ckm = cnt_ge(km);
       if (ckm == K) {
         lo = km - 1;   // exactly the K largest: tau = km
         hi = km;
       } else {
         lo = km;       // cnt(km) > K
-        CTCX_LDS unsigned* cks = (CTCX_LDS unsigned*)(plds + (INLDS ? ((size_t)C * sizeof(T) + 15) & ~(size_t)15 : 0));
+        CTCX_LDS unsigned* cks =
+            (CTCX_LDS unsigned*)(plds + kPrepTabBytes + (INLDS ? ((size_t)C * sizeof(T) + 15) & ~(size_t)15 : 0));
         if (ckm <= kPrepCompact) {
           // every key >= km into a compact list (at most kPrepCompact), then
           // bisect in registers: tau > km, so S lies in the list
@@ -3355,9 +3402,7 @@ __global__ __launch_bounds__(64) void ctcx_row_prep(const T* __restrict__ x, con
             int c = 0;
 #pragma unroll
             for (int q = 0; q < kPrepCompact / 64; ++q) c += ck[q] >= (unsigned)mid ? 1 : 0;
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o);
-            c = uni(c);
+            c = uni(wave_sum_dpp(c));
             if (c <= K) hi = mid;
             else lo = mid;
             if (c == K) break;
@@ -3394,7 +3439,7 @@ __global__ __launch_bounds__(64) void ctcx_row_prep(const T* __restrict__ x, con
       n += __builtin_popcountll(m);
     }
     h.ns = n;
-    h.xout = wave_max(xo);
+    h.xout = wave_max_dpp(xo);
   }
   if (lane == 0) *(RowHdr<T>*)pr = h;
   // the normaliser: m = the row maximum -- in class order when a NaN is
@@ -3411,7 +3456,10 @@ __global__ __launch_bounds__(64) void ctcx_row_prep(const T* __restrict__ x, con
   T ssum = T(0);
   if (inlds) {
     __syncthreads();
-    for (int j = lane; j < Ci; j += 64) xs[j] = norm_exp(xs[j] - m);
+    for (int j = lane; j < Ci; j += 64) {
+      if constexpr (sizeof(T) == 4) xs[j] = gm::expf_t(xs[j] - m, etab);   // glibc expf, its table in LDS
+      else xs[j] = norm_exp(xs[j] - m);
+    }
     __syncthreads();
     if (lane == 0) {
       int j = 0;
@@ -3667,10 +3715,11 @@ hipError_t launch_row_prep(const T* x, const int32_t* sl, char* prep, T* norm, i
   const int64_t rows = T_ * B;
   if (rows == 0 || C <= 64) return hipSuccess;
   const size_t row_b = (size_t)C * sizeof(T);
-  const size_t lds = ((row_b + 15) & ~(size_t)15) + 4 * kPrepCompact;   // the row, then the compact key list
+  // the expf table, the row, then the compact key list
+  const size_t lds = kPrepTabBytes + ((row_b + 15) & ~(size_t)15) + 4 * kPrepCompact;
   if (row_b > kPrepLdsBytes) {   // the row is read from global memory
-    hipLaunchKernelGGL((ctcx_row_prep<T, false>), dim3((unsigned)rows), dim3(64), 4 * kPrepCompact, s, x, sl, prep,
-                       norm, B, C, xstride, blank);
+    hipLaunchKernelGGL((ctcx_row_prep<T, false>), dim3((unsigned)rows), dim3(64), kPrepTabBytes + 4 * kPrepCompact,
+                       s, x, sl, prep, norm, B, C, xstride, blank);
     return hipGetLastError();
   }
   if (lds > 64 * 1024) {

@@ -67,7 +67,11 @@ CTCX_HD uint64_t exp2f_tab(int i) {
   }
 }
 
-CTCX_HD float expf(float x) {
+// Tab: i -> 2^(i/32) bits as exp2f_tab gives them.  expf uses the switch
+// (no memory object); a caller whose lanes take divergent indices (a switch
+// is then a branch per case) passes a copy of the table in LDS (expf_t).
+template <class Tab>
+CTCX_HD float expf_impl(float x, const Tab& tab) {
   const uint32_t ux = f2u(x);
   const uint32_t abstop = (ux >> 20) & 0x7ff;
   if (abstop >= 0x42bu) {                  // |x| >= 88 or nan
@@ -87,7 +91,7 @@ CTCX_HD float expf(float x) {
   const uint64_t ki = d2u(kd);
   kd -= Shift;
   const double r = __builtin_fma(InvLn2N, xd, -kd);
-  uint64_t t = exp2f_tab((int)(ki % 32));
+  uint64_t t = tab((int)(ki % 32));
   t += ki << 47;
   const double s = u2d(t);
   const double zc = __builtin_fma(0x1.c6af84b912394p-20, r, 0x1.ebfce50fac4f3p-13);
@@ -96,6 +100,13 @@ CTCX_HD float expf(float x) {
   y = __builtin_fma(zc, r2, y);
   y = y * s;
   return (float)y;
+}
+CTCX_HD float expf(float x) {
+  return expf_impl(x, [](int i) { return exp2f_tab(i); });
+}
+template <class P>
+CTCX_HD float expf_t(float x, P tab) {   // tab[i] == exp2f_tab(i), e.g. in LDS
+  return expf_impl(x, [tab](int i) { return (uint64_t)tab[i]; });
 }
 
 // ---- logf ------------------------------------------------------------------
