@@ -39,7 +39,7 @@ CONFIGS = {
     "cfg5": (512, 3000, 5000, 256, 1, False, 0),
 }
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# Calibration of the CPU baseline (BASELINE.md "Calibration"): the oracle's
+# Calibration of the CPU baseline (BASELINE.md "Calibration of the CPU baseline"): the oracle's
 # reference-cost mode ("port") timed in the build container on SURVEY.md 6's
 # cfg3-shape item (C=29, W=128, P=3, T=1500, merge) ran 81-104 frames/s per
 # core (median of 5 runs ~88) against the compiled reference's 189 frames/s
@@ -379,6 +379,8 @@ def main():
         if tcap < T:
             res["cpu_baseline"]["truncated"] = "T=%d of %d (BASELINE.md: full items do not fit host memory)" % (tcap, T)
         res["cpu_baseline"]["gpu_over_cpu"] = value / res["cpu_baseline"]["value"]
+        res["cpu_baseline"]["calibration"]["gpu_over_reference_equivalent"] = (
+            value / res["cpu_baseline"]["calibration"]["reference_equivalent_value"])
         res["cpu_baseline"]["host_cpus"] = info
     if rank == 0:
         print(json.dumps(res), flush=True)

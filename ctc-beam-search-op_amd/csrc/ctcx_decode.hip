@@ -58,12 +58,15 @@ template <> __host__ __device__ __forceinline__ float pinf<float>() { return __b
 template <> __host__ __device__ __forceinline__ double pinf<double>() { return __builtin_inf(); }
 
 // util/ctc_loss_util.h:29-41 — float libm (expf, log1pf) even for T=double.
-template <typename T>
-__host__ __device__ __forceinline__ T lse(T a, T b) {
+// etab: expf's 2^(i/32) table (a copy in LDS: lanes that run the recursion
+// in parallel take divergent table indices, and the switch form would branch
+// once per case)
+template <typename T, class P>
+__host__ __device__ __forceinline__ T lse(T a, T b, P etab) {
   if (a == ninf<T>()) return b;
   if (b == ninf<T>()) return a;
-  return (a > b) ? a + (T)gm::log1pf(gm::expf((float)(b - a)))
-                 : b + (T)gm::log1pf(gm::expf((float)(a - b)));
+  return (a > b) ? a + (T)gm::log1pf(gm::expf_t((float)(b - a), etab))
+                 : b + (T)gm::log1pf(gm::expf_t((float)(a - b), etab));
 }
 
 __device__ __forceinline__ float bcast(float v, int k) {
@@ -231,6 +234,7 @@ struct Ctx {
   CTCX_LDS int* htab;
   CTCX_LDS uint64_t* bloom;   // per branch: label bits (l & 63) of children evicted this frame
   CTCX_LDS HE<T>* he;  // TopN elements_, position p at he[p + 1]
+  CTCX_LDS uint64_t* etab;   // expf's 2^(i/32) table (gm::exp2f_tab), for lse
   // beam-scorer state (a stateful scorer only): per branch [buf][i], per entry
   CTCX_LDS T* est[2]; CTCX_LDS T* eest;
   const T* sctab;      // the scorer's table (global memory)
@@ -356,6 +360,7 @@ __host__ __device__ __forceinline__ void carve(Ctx<T>& cx, CTCX_LDS char* base, 
   cx.sorted = (CTCX_LDS int*)p; p += a16((size_t)Wcap * 4);
   cx.alias = (CTCX_LDS int*)p; p += a16((size_t)Wcap * 4);
   cx.misc = (CTCX_LDS int*)p; p += 64;
+  cx.etab = (CTCX_LDS uint64_t*)p; p += 32 * 8;
   for (int b = 0; b < nbuf; ++b) {
     CTCX_LDS uint64_t* q = (CTCX_LDS uint64_t*)p;
     cx.ha[b] = q; cx.hb[b] = q + Wcap;
@@ -460,7 +465,7 @@ __host__ __device__ __forceinline__ void recurse_branch(const Ctx<T>& cx, int bu
       const bool same = (L == sel(cx.lab, buf)[P]);
       T prev = same ? sel(cx.ob, buf)[P] : sel(cx.ot, buf)[P];
       if constexpr (SC::kStateful) prev = SC::score(sel(cx.est, buf)[i], prev);
-      nl = lse(nl, prev) + xl - norm;
+      nl = lse(nl, prev, cx.etab) + xl - norm;
       cand_from(cx, buf, P, 0, p, rs_blank, bn);
       if (!same) cand_from(cx, buf, P, 1, p, NI, bn);
       cand_from(cx, buf, i, 1, p, NI, bn);
@@ -485,7 +490,7 @@ __host__ __device__ __forceinline__ void recurse_branch(const Ctx<T>& cx, int bu
   cand_from(cx, buf, i, 1, pb, NI, bb);
   cx.eb[e] = nbk;
   cx.el[e] = nl;
-  cx.et[e] = lse(nbk, nl);
+  cx.et[e] = lse(nbk, nl, cx.etab);
   cx.ecb[e] = bb.p; cx.ebpb[e] = bb.bp;
   cx.ecn[e] = bn.p; cx.ebpn[e] = bn.bp;
   cx.eflg[e] = (bb.ok ? F_HB : 0) | (bn.ok ? F_HN : 0);
@@ -2904,6 +2909,7 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
 
   // Reset(): root with newp.total = newp.blank = 0 (decoder.h:213-227)
   int buf = 0;
+  if (lane < 32) cx.etab[lane] = gm::exp2f_tab(lane);
   if (lane == 0) {
     cx.lab[0][0] = -1; cx.par[0][0] = -1; cx.flg[0][0] = F_ROOT;
     cx.ot[0][0] = T(0); cx.ob[0][0] = T(0); cx.ol[0][0] = ninf<T>();

@@ -183,6 +183,7 @@ __host__ __device__ inline size_t decode_lds_bytes(int W, int64_t C, int tsize, 
   s += a16((size_t)W * 4);                      // sorted
   s += a16((size_t)W * 4);                      // alias (entries the beam holds twice)
   s += 64;                                      // scalars
+  s += 32 * 8;                                  // expf's 2^(i/32) table
   s += nbuf * 2 * (size_t)W * 8;                // prefix hashes (two 64-bit chains)
   s += a16(4 * (size_t)htab_size(W));           // per-frame new-leaf hash table  } the free list / slot
   s += a16(8 * (size_t)W);                      // per-branch evicted-child bloom } map aliases these two
