@@ -30,10 +30,16 @@ FAMILIES = {
     "large_c_ties": (5009, dict(T_max=30, B_max=2, C_min=65, C_max=400, W_min=8, W_max=256, ties=True)),
     "neg_inf": (5010, dict(T_max=30, B_max=3, C_max=20, W_max=40, neg_inf=True)),
     "f64_mixed": (5011, dict(T_max=30, B_max=2, C_max=200, W_max=150, dtype=np.float64)),
+    # round 3: C above 2048 (pre-pass rows, compacted gather), and the
+    # global-state tier forced onto small mixed cases
+    "large_c_2k": (5012, dict(T_max=14, B_max=2, C_min=2049, C_max=3000, W_min=32, W_max=256)),
+    "gstate_mixed": (5013, dict(T_max=30, B_max=2, C_max=80, W_max=60, flags="gstate")),
 }
 total = 0
 t0 = time.time()
 for name, (seed, kw) in FAMILIES.items():
+    kw = dict(kw)
+    flags = ctcext_amd._lib.CTCEXT_FLAG_GLOBAL_STATE if kw.pop("flags", None) == "gstate" else 0
     rng = np.random.default_rng(seed)
     n_err = 0
     for it in range(N):
@@ -43,7 +49,7 @@ for name, (seed, kw) in FAMILIES.items():
         try:
             xin = torch.as_tensor(x, device="cuda:0") if dev else x
             slin = torch.as_tensor(sl, device="cuda:0") if dev else sl
-            out = ctcext_amd.ctc_ext_beam_search_decoder(xin, slin, W, P, **akw)
+            out = ctcext_amd.ctc_ext_beam_search_decoder(xin, slin, W, P, flags=flags, **akw)
             torch.cuda.synchronize()
             gerr = None
         except ctcext_amd.OpError as e:   # the op's InvalidArgument / FailedPrecondition
