@@ -33,3 +33,12 @@ for k in range(24):
     print("  %-10s %12.0f %s/frame" % (names[k], m[k] / fr, "cycles" if k in CYC else "count"))
 if m[6] > 0:
     print("  asm loop cycles per push (incl. entry/exit): %.0f" % (m[13] / m[6]))
+# per item: the kernel ends with its slowest item (one wave per item)
+tot = buf[:, [0, 1, 2, 3, 4, 5]].astype(np.float64).sum(1)
+o = np.argsort(tot)
+print("  per-item cycles/frame: min %.0f mean %.0f max %.0f (items %s slowest)" % (
+    tot.min() / fr, tot.mean() / fr, tot.max() / fr, list(o[-4:][::-1])))
+for b in o[-3:][::-1]:
+    print("    item %d: heap events %.0f/frame, extract %.0f, grow %.0f, eventloop %.0f, scoring %.0f" % (
+        b, buf[b, 6] / fr, buf[b, 3] / fr, buf[b, 2] / fr, buf[b, 9] / fr, buf[b, 8] / fr))
+print("  mean heap events/frame %.1f, max %.1f" % (buf[:, 6].mean() / fr, buf[:, 6].max() / fr))
