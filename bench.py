@@ -224,6 +224,8 @@ def main():
     ap.add_argument("--no-host-io", action="store_true", help="skip the host-I/O (PCIe-inclusive) extra")
     ap.add_argument("--seq-len", type=int, default=0, help="diagnostics: override T (not a bench line)")
     ap.add_argument("--batch-per-gpu", type=int, default=0, help="diagnostics: override B per GPU (not a bench line)")
+    ap.add_argument("--record-ring", action="store_true",
+                    help="diagnostics: the LDS record ring (only reachable beam records written to HBM)")
     ap.add_argument("--no-strong", action="store_true",
                     help="skip the strong-scaling extra (N=1: the per-GPU latency at the B=256/N shards; "
                          "N>1: the measured global-B=256 split)")
@@ -263,7 +265,7 @@ def main():
     sl = torch.as_tensor(sl_np, device=dev)
     torch.cuda.synchronize()
 
-    flags = _lib.CTCEXT_FLAG_PROFILE
+    flags = _lib.CTCEXT_FLAG_PROFILE | (_lib.CTCEXT_FLAG_RECORD_RING if args.record_ring else 0)
     dec = ctcext_amd.get_decoder(local)
 
     def step(outputs="host"):
@@ -336,7 +338,10 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "ctcx_beam_decode", "kernel_ms": kavg,
-                     "algorithmic_bytes_per_launch": abytes},
+                     "algorithmic_bytes_per_launch": abytes,
+                     # beam records the decode kernel wrote to HBM (8 B each; with the
+                     # LDS record ring only those the traceback can reach)
+                     "record_ring_frames": st["ring_frames"], "records_written": st["records_written"]},
         "literal_frames_per_step": lit / max(args.steps, 1),
         "lib_sha16": lib_hash(),
         "what": ("one decode call: device logits in, int64 SparseTensor components materialised on the host"

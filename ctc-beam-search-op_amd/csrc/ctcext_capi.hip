@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -22,6 +23,8 @@
 namespace ctcx {
 template <typename T>
 hipError_t launch_decode(const DecodeParams<T>& p, hipStream_t s);
+template <typename T>
+int ring_frames(const DecodeParams<T>& p, int cus, int cap);
 template <typename T>
 hipError_t launch_row_norm(const T* x, const int32_t* sl, T* norm, int64_t T_, int64_t B, int64_t C,
                            int64_t xstride, hipStream_t s);
@@ -111,8 +114,10 @@ struct Dev {
   hipStream_t own_stream = nullptr;
   hipStream_t s = nullptr;   // stream of the current call
   hipEvent_t ev[4] = {};
-  DevBuf x, sl, norm, prep, rec, item, top_pos, top_kind, logp, seq, len, phase, sctab, gstate;
+  DevBuf x, sl, norm, prep, rec, foff, item, top_pos, top_kind, logp, seq, len, phase, sctab, gstate;
   int64_t lo = 0, nb = 0;    // this call's shard [lo, lo + nb)
+  int ring = 0;              // this call's record-ring frames (ctcx::ring_frames)
+  int cus = 0;               // compute units of the device
 };
 
 }  // namespace
@@ -134,7 +139,7 @@ struct ctcext_decoder {
 static void release_dev(Dev& d) {
   (void)hipSetDevice(d.device);
   if (d.own_stream) (void)hipStreamSynchronize(d.own_stream);
-  DevBuf* bufs[] = {&d.x, &d.sl, &d.norm, &d.prep, &d.rec, &d.item, &d.top_pos, &d.top_kind, &d.logp,
+  DevBuf* bufs[] = {&d.x, &d.sl, &d.norm, &d.prep, &d.rec, &d.foff, &d.item, &d.top_pos, &d.top_kind, &d.logp,
                     &d.seq, &d.len, &d.phase, &d.sctab, &d.gstate};
   for (DevBuf* b : bufs) b->release();
   for (auto& ev : d.ev)
@@ -415,6 +420,19 @@ static int enqueue_shard(ctcext_decoder* d, Dev& v, bool root, const ctcext_deco
   // the host checked the shapes the kernel's grid and LDS carve assume
   if (Bs > 0x7fffffffLL || (!gs && (W > ctcx::kMaxRecBeam || C > ctcx::kMaxRecClasses)))
     return fail(CTCEXT_INTERNAL, "shard shape outside the kernel's limits");
+  v.ring = 0;
+  if (!gs && (a->flags & (CTCEXT_FLAG_RECORD_RING | CTCEXT_FLAG_RING_MIN))) {
+    if (v.cus == 0 && hipDeviceGetAttribute(&v.cus, hipDeviceAttributeMultiprocessorCount, v.device) != hipSuccess)
+      v.cus = 1;
+    // CTCEXT_RING_FRAMES (diagnostics): a smaller ring cap than the default 64
+    const char* rc = getenv("CTCEXT_RING_FRAMES");
+    const int cap = (a->flags & CTCEXT_FLAG_RING_MIN) ? 8 : (rc && atoi(rc) >= 8) ? std::min(atoi(rc), 256) : 64;
+    p.ring = v.ring = ctcx::ring_frames<T>(p, v.cus, cap);
+    if (p.ring > 0) {
+      HIP_OR_FAIL(v.foff.ensure(4 * (size_t)(Bs * T_)));
+      p.foff = (int32_t*)v.foff.p;
+    }
+  }
   if (gs) {
     p.gstate = (char*)v.gstate.p;
     p.gstate_stride = (int64_t)ctcx::gstate_bytes(W, (int)sizeof(T), scored);
@@ -429,6 +447,7 @@ static int enqueue_shard(ctcext_decoder* d, Dev& v, bool root, const ctcext_deco
   tp.Tmax = T_; tp.B = Bs; tp.W = W; tp.P = P; tp.merge = a->merge_repeated ? 1 : 0;
   tp.blank_label = a->blank_label;
   tp.rec_wide = gs ? 1 : 0;
+  tp.foff = p.foff;
   tp.seq = (int32_t*)v.seq.p;
   tp.len = (int32_t*)v.len.p;
   tp.len_stride = Bo;
@@ -530,6 +549,7 @@ static int run_decode(ctcext_decoder* d, const ctcext_decode_args* a, const std:
 
   d->stats = ctcext_stats{};
   d->stats.tier = use_gstate(a) ? 1 : 0;
+  d->stats.ring_frames = root.ring;
   if (a->flags & CTCEXT_FLAG_PROFILE) {
     for (int i = 0; i < nd; ++i) {
       Dev& v = d->devs[(size_t)i];
@@ -549,6 +569,7 @@ static int run_decode(ctcext_decoder* d, const ctcext_decode_args* a, const std:
     d->stats.literal_nonfinite += io[b].why_nonfinite;
     d->stats.literal_fill += io[b].why_fill;
     d->stats.duplicate_frames += io[b].dup_frames;
+    d->stats.records_written += io[b].records;
   }
   // TopPaths (decoder.h:240-243) fails on the first item with too few leaves
   for (int64_t b = 0; b < B; ++b)

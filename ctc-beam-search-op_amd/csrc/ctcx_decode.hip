@@ -2885,6 +2885,154 @@ __host__ __device__ __attribute__((noinline)) int literal_step(Ctx<T> cx, int bu
 }
 
 // ---------------------------------------------------------------------------
+// Record ring (LDS tier).  The traceback reads back only the P final paths'
+// record chains (ctcx_traceback), and the chains of a frame's beams merge a
+// few frames back: the beams share prefixes (the link) and alignment
+// candidates (the two back-pointers).  Writing all W records of every frame
+// (T·W·8 B per item, 393 MB per cfg3 launch) spends HBM writes on records
+// nothing reads.  So the commit writes a frame's records into an LDS ring of
+// R frames instead, and every R/2 frames ring_flush marks the records
+// reachable from the current beam back through the ring (frame by frame: a
+// reachable record's link and back-pointers mark their targets one frame
+// down) and appends the reachable records of the oldest R/2 frames to the
+// item's record stream in HBM, compacted, their pointers renumbered to the
+// targets' compacted positions (frame u's records start at foff[u]).  A
+// record unreachable now stays unreachable: every later beam descends from a
+// current one.  After the last frame the walk starts from the TopPaths
+// positions alone, and their compacted positions are what top_pos reports.
+struct Ring {
+  CTCX_LDS Rec* rec;        // [R][W]: frame u in row u & (R - 1)
+  CTCX_LDS int* rn;         // [R]: entries of each ring frame
+  CTCX_LDS int16_t* tbl;    // [2][W]: compacted positions, by frame parity
+  CTCX_LDS int16_t* sv;     // [2][W]: the newest written frame's, by flush parity
+  CTCX_LDS int* st;         // [2][W]: reachability stamps, by frame parity
+  int R, W;
+};
+
+__device__ __forceinline__ Ring ring_carve(CTCX_LDS char* p, int R, int W) {
+  auto a16 = [](size_t v) { return (v + 15) & ~(size_t)15; };
+  Ring g;
+  g.R = R;
+  g.W = W;
+  g.rec = (CTCX_LDS Rec*)p; p += (size_t)R * W * 8;
+  g.rn = (CTCX_LDS int*)p; p += a16(4 * (size_t)R);
+  g.tbl = (CTCX_LDS int16_t*)p; p += a16(4 * (size_t)W);
+  g.sv = (CTCX_LDS int16_t*)p; p += a16(4 * (size_t)W);
+  g.st = (CTCX_LDS int*)p;
+  return g;
+}
+
+// Reachable positions (a[j]: position lane + 64 j) -> compacted positions
+// (rk[j]), in position order; returns how many there are.
+template <int KM>
+__device__ __forceinline__ int ring_rank(const bool (&a)[KM], int (&rk)[KM]) {
+  int base = 0;
+#pragma unroll
+  for (int j = 0; j < KM; ++j) {
+    const uint64_t m = __ballot(a[j]);
+    rk[j] = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+    base += __builtin_popcountll(m);
+  }
+  return base;
+}
+
+// Marks from frame t_new (every entry, or the tops positions) down to u_lo,
+// the oldest frame in the ring, and writes frames u_hi .. u_lo (reachable
+// records, compacted) to the stream at out + cursor on.  fp: this flush's
+// number (the previous flush left frame u_lo - 1's compacted positions in
+// sv[(fp - 1) & 1]; this one leaves frame u_hi's in sv[fp & 1]).  Lane L
+// holds positions L + 64 j (j < KM, KM * 64 >= W): their reachability, compacted
+// positions and records stay in registers; a frame's reachable records stamp
+// their targets one frame down (a value unique to this flush and step, so the
+// stamps need no clearing), and the compacted positions go to LDS for the
+// renumbering gathers.
+template <int KM>
+__device__ void ring_flush(const Ring& g, Rec* out, int32_t* foff, int t_new, int u_lo, int u_hi,
+                           const CTCX_LDS int* tops, int ntops, int fp, int& cursor) {
+  const int lane = threadIdx.x, M = g.R - 1, W = g.W;
+  const int sbase = fp * 4096;   // stamps of this flush: sbase + (t_new - frame) + 1; R <= 256
+  bool al[KM];
+  int rk[KM];
+  {
+    const int n = g.rn[t_new & M];
+    if (tops != nullptr) {
+      for (int q = lane; q < ntops; q += 64) g.st[(t_new & 1) * W + tops[q]] = sbase;
+      __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < KM; ++j) {
+      const int k = lane + 64 * j;
+      al[j] = k < n && (tops == nullptr || g.st[(t_new & 1) * W + k] == sbase);
+    }
+  }
+  int cnt = ring_rank<KM>(al, rk);
+  for (int u = t_new; u >= u_lo; --u) {
+    const CTCX_LDS Rec* ru = g.rec + (size_t)(u & M) * W;
+    Rec r[KM];
+#pragma unroll
+    for (int j = 0; j < KM; ++j) r[j] = al[j] ? ru[lane + 64 * j] : 0ull;
+    bool al1[KM];
+    int rk1[KM], cnt1 = 0;
+    if (u > u_lo) {
+      // frame u - 1: the targets of frame u's reachable records
+      CTCX_LDS int* s1 = g.st + ((u - 1) & 1) * W;
+      const int sv1 = sbase + (t_new - u) + 1;
+#pragma unroll
+      for (int j = 0; j < KM; ++j) {
+        if (al[j]) {
+          const uint32_t qb = rec_bp_blank(r[j]), qn = rec_bp_nblank(r[j]);
+          s1[rec_link(r[j]) >> 1] = sv1;
+          if (qb < kBpRestart) s1[qb >> 1] = sv1;
+          if (qn < kBpRestart) s1[qn >> 1] = sv1;
+        }
+      }
+      __syncthreads();
+      const int n1 = g.rn[(u - 1) & M];
+#pragma unroll
+      for (int j = 0; j < KM; ++j) {
+        const int k = lane + 64 * j;
+        al1[j] = k < n1 && s1[k] == sv1;
+      }
+      cnt1 = ring_rank<KM>(al1, rk1);
+      if (u <= u_hi) {
+        CTCX_LDS int16_t* t1 = g.tbl + ((u - 1) & 1) * W;
+#pragma unroll
+        for (int j = 0; j < KM; ++j)
+          if (al1[j]) t1[lane + 64 * j] = (int16_t)rk1[j];
+        __syncthreads();
+      }
+    }
+    if (u <= u_hi) {
+      if (u == u_hi) {
+#pragma unroll
+        for (int j = 0; j < KM; ++j)
+          if (al[j]) g.sv[(fp & 1) * W + lane + 64 * j] = (int16_t)rk[j];
+      }
+      // the targets' compacted positions: frame u - 1 in the ring, or written
+      // by the previous flush; frame 0's targets are the root (left as they are)
+      const CTCX_LDS int16_t* tp = u > u_lo ? g.tbl + ((u - 1) & 1) * W : g.sv + ((fp - 1) & 1) * W;
+#pragma unroll
+      for (int j = 0; j < KM; ++j) {
+        if (al[j]) {
+          uint32_t lk = rec_link(r[j]), qb = rec_bp_blank(r[j]), qn = rec_bp_nblank(r[j]);
+          if (u > 0) {
+            lk = ((uint32_t)tp[lk >> 1] << 1) | (lk & 1u);
+            if (qb < kBpRestart) qb = ((uint32_t)tp[qb >> 1] << 1) | (qb & 1u);
+            if (qn < kBpRestart) qn = ((uint32_t)tp[qn >> 1] << 1) | (qn & 1u);
+          }
+          out[cursor + rk[j]] = rec_pack(lk, rec_label(r[j]), qb, qn);
+        }
+      }
+      if (lane == 0) foff[u] = cursor;
+      cursor += cnt;
+    }
+#pragma unroll
+    for (int j = 0; j < KM; ++j) { al[j] = al1[j]; rk[j] = rk1[j]; }
+    cnt = cnt1;
+  }
+  __syncthreads();
+}
+
 template <typename T, int RN, int WC, bool BIG, class SC>
 __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
   Ctx<T> cx;
@@ -2906,6 +3054,20 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
   const int64_t B = prm.B;
   const int sl = prm.seq_len[b] > 0 ? prm.seq_len[b] : 0;
   CTCX_LDS int* const misc = cx.misc;
+  // the record ring (host: ring_frames) after the decode layout; R = 0 writes
+  // every record to rec[b][t][k]
+  const int R = prm.ring;
+  Ring rg{};
+#ifndef CTCX_GSTATE
+  if (R > 0)
+    rg = ring_carve((CTCX_LDS char*)lds + ((decode_lds_bytes(WC > 0 ? WC : W, C, (int)sizeof(T), SC::kStateful) +
+                                            15) & ~(size_t)15), R, W);
+#endif
+  if (R > 0)
+    for (int k = lane; k < 2 * W; k += 64) rg.st[k] = -1;   // no stamp yet
+  Rec* const rstream = prm.rec + b * prm.Tmax * W;   // item b's record stream (ring)
+  int32_t* const foff = prm.foff ? prm.foff + b * prm.Tmax : nullptr;
+  int flushed = 0, nflush = 0, nrec = 0;   // first frame not yet in HBM, flushes, records written
 
   // Reset(): root with newp.total = newp.blank = 0 (decoder.h:213-227)
   int buf = 0;
@@ -3092,7 +3254,8 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
 #ifdef CTCX_GSTATE
       ((Rec16*)prm.rec)[((int64_t)b * prm.Tmax + t) * W + k] = Rec16{kd, cx.elab[e], bpb, bpn};
 #else
-      prm.rec[((int64_t)b * prm.Tmax + t) * W + k] = rec_pack(kd, cx.elab[e], bpb, bpn);
+      if (R > 0) rg.rec[(t & (R - 1)) * W + k] = rec_pack(kd, cx.elab[e], bpb, bpn);
+      else prm.rec[((int64_t)b * prm.Tmax + t) * W + k] = rec_pack(kd, cx.elab[e], bpb, bpn);
 #endif
     };
     if constexpr (STAGED) {
@@ -3133,6 +3296,7 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
         put_branch(k, parent, fl);
       }
     }
+    if (R > 0 && lane == 0) rg.rn[t & (R - 1)] = n;
     __syncthreads();
     buf = nx;
     nb = n;
@@ -3144,6 +3308,12 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
       if (pp >= 0 && (!dup || cx.alias[k] == k))
         cx.sib[k] = __hip_atomic_exchange(&cx.head[pp], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+    if (R == 0) nrec += n;
+    else if (t - flushed + 1 == R) {   // the ring is full: write its older half
+      ring_flush<KM>(rg, rstream, foff, t, flushed, flushed + R / 2 - 1, nullptr, 0, nflush, nrec);
+      flushed += R / 2;
+      ++nflush;
+    }
     __syncthreads();
     if (prof) { pc[4] += __builtin_amdgcn_s_memtime() - t3; pc[7] += 1; }
   }
@@ -3154,11 +3324,14 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
   if (sl == 0 && lane == 0) cx.tops[0] = 0;
   __syncthreads();
   const int np = (prm.P < n_leaves) ? prm.P : n_leaves;
+  // the rest of the ring, walked from the TopPaths positions
+  if (R > 0 && sl > 0) ring_flush<(WC > 0 ? WC : 512) / 64>(rg, rstream, foff, sl - 1, flushed, sl - 1, cx.tops, np, nflush, nrec);
   for (int q = lane; q < prm.P; q += 64) {
-    int pos = -1, kind = -1;
+    int pos = -1, kind = -1, opos = -1;
     T lp = T(0);
     if (q < np) {
       pos = cx.tops[q];
+      opos = (R > 0 && sl > 0) ? (int)rg.sv[(nflush & 1) * W + pos] : pos;   // its record's stream position
       const int f = sel(cx.flg, buf)[pos];
       const bool hb = f & F_HB, hn = f & F_HN;
       if (hb && hn) kind = (sel(cx.cb, buf)[pos] > sel(cx.cn, buf)[pos]) ? 0 : 1;
@@ -3166,7 +3339,7 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
       else if (hn) kind = 1;
       lp = sel(cx.ot, buf)[pos];
     }
-    prm.top_pos[b * prm.P + q] = pos;
+    prm.top_pos[b * prm.P + q] = opos;
     prm.top_kind[b * prm.P + q] = kind;
     prm.log_prob[b * prm.P + q] = lp;
   }
@@ -3177,7 +3350,8 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     io.dup_frames = dup_frames;
     io.why_nonfinite = why_nf;
     io.why_fill = why_fill;
-    io.pad[0] = io.pad[1] = io.pad[2] = 0;
+    io.records = nrec;
+    io.pad[0] = io.pad[1] = 0;
     prm.item[b] = io;
   }
 }
@@ -3503,7 +3677,7 @@ __global__ __launch_bounds__(256) void ctcx_traceback(TraceParams tp) {
   if (sl > 0 && k >= 0 && p < tp.item[b].n_leaves) {
     // record (t, k) unpacked: link, label, the two alignment back-pointers
     auto rd = [&](int t, uint32_t& link, int& lab, uint32_t& bpb, uint32_t& bpn) {
-      const int64_t at = (b * tp.Tmax + t) * tp.W + k;
+      const int64_t at = tp.foff ? b * tp.Tmax * tp.W + tp.foff[b * tp.Tmax + t] + k : (b * tp.Tmax + t) * tp.W + k;
       if (tp.rec_wide) {
         const Rec16 r = ((const Rec16*)tp.rec)[at];
         link = r.link; lab = r.label; bpb = r.bpb; bpn = r.bpn;
@@ -3602,7 +3776,8 @@ namespace ctcx {
 
 template <typename T, int RN, int WC, bool BIG, class SC>
 hipError_t launch_decode_c(const DecodeParams<T>& p, hipStream_t s) {
-  const size_t lds = decode_lds_bytes(WC > 0 ? WC : p.W, p.C, (int)sizeof(T), SC::kStateful);
+  size_t lds = decode_lds_bytes(WC > 0 ? WC : p.W, p.C, (int)sizeof(T), SC::kStateful);
+  if (p.ring > 0) lds = ((lds + 15) & ~(size_t)15) + ring_lds_bytes(p.ring, p.W);
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)ctcx_beam_decode<T, RN, WC, BIG, SC>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -3714,6 +3889,26 @@ hipError_t launch_decode(const DecodeParams<T>& p, hipStream_t s) {
 
 template hipError_t launch_decode<float>(const DecodeParams<float>&, hipStream_t);
 template hipError_t launch_decode<double>(const DecodeParams<double>&, hipStream_t);
+
+// Frames of the record ring for launch_decode's choice of kernel (0: none):
+// the largest power of two in [8, cap] whose ring fits beside the decode
+// layout: within the CU's LDS when the batch has at most one item per CU (or
+// the layout alone already takes more than half a CU), else within 80 KB, so
+// two items still share a CU.  The stream offsets (foff) are int32.
+template <typename T>
+int ring_frames(const DecodeParams<T>& p, int cus, int cap) {
+  const bool scored = p.scorer_tab != nullptr;
+  auto fits = [&](int wc) { return decode_lds_bytes(wc, p.C, (int)sizeof(T), scored) <= kLdsBytes; };
+  const int wcap = (p.W <= 128 && fits(128)) ? 128 : (p.W > 128 && p.W <= 256 && fits(256)) ? 256 : p.W;
+  if ((int64_t)p.Tmax * p.W > 0x7fffffffLL) return 0;
+  const size_t base = (decode_lds_bytes(wcap, p.C, (int)sizeof(T), scored) + 15) & ~(size_t)15;
+  const size_t budget = (base > 80 * 1024 || p.B <= cus) ? kLdsBytes : 80 * 1024;
+  for (int r = cap; r >= 8; r >>= 1)
+    if (base + ring_lds_bytes(r, p.W) <= budget) return r;
+  return 0;
+}
+template int ring_frames<float>(const DecodeParams<float>&, int, int);
+template int ring_frames<double>(const DecodeParams<double>&, int, int);
 
 template <typename T>
 hipError_t launch_row_prep(const T* x, const int32_t* sl, char* prep, T* norm, int64_t T_, int64_t B, int64_t C,

@@ -65,7 +65,8 @@ struct ItemOut {
   int32_t dup_frames;     // frames whose beam held one entry twice (-inf logits)
   int32_t why_nonfinite;  // literal replays caused by a non-finite logit or total
   int32_t why_fill;       // ... by the beam filling up mid-frame
-  int32_t pad[3];
+  int32_t records;        // records written to HBM (all of them without the record ring)
+  int32_t pad[2];
 };
 
 // Large C (> 64): per-(t, b) row facts computed by the parallel pre-pass
@@ -118,6 +119,11 @@ struct DecodeParams {
   // written as Rec16 through rec
   char* gstate;
   int64_t gstate_stride;
+  // record ring (LDS tier, ring_frames): frames of records kept in LDS (0: every
+  // record written to rec[b][t][k] directly); with it item b's records form a
+  // compacted stream at rec + b * Tmax * W, frame t's from foff[b][t] on
+  int32_t ring;
+  int32_t* foff;            // [B][Tmax]
 };
 
 struct TraceParams {
@@ -129,6 +135,7 @@ struct TraceParams {
   int64_t Tmax, B;
   int32_t W, P, merge, blank_label;
   int32_t rec_wide;   // records are Rec16 (global-state tier), else Rec
+  const int32_t* foff;   // record ring: frame t of item b at rec + b * Tmax * W + foff[b][t] (null: [b][t][W])
   int32_t* seq;    // [B][P][2][Tmax]  walk output, reversed
   int32_t* len;    // [P][2][len_stride], this batch's items at [.][.][0, B)
   int64_t len_stride;
@@ -166,6 +173,15 @@ constexpr size_t kLdsBytes = 160 * 1024;   // LDS per CU on gfx950 (one workgrou
 // per-frame commit updates in place (the row of C values takes the room; two
 // items then fit one CU at cfg5).  C <= 64: two buffers, by frame parity.
 __host__ __device__ inline bool decode_inplace(int64_t C) { return C > 64; }
+
+// LDS bytes of the record ring of R frames (after the decode layout, 16-byte
+// aligned): the records [R][W], entries per frame [R], compacted positions by
+// frame parity [2][W] and of the newest written frame by flush parity [2][W]
+// (int16), reachability stamps by frame parity [2][W] (int32).
+__host__ __device__ inline size_t ring_lds_bytes(int R, int W) {
+  auto a16 = [](size_t v) { return (v + 15) & ~(size_t)15; };
+  return (size_t)R * (size_t)W * 8 + a16(4 * (size_t)R) + 2 * a16(4 * (size_t)W) + a16(8 * (size_t)W);
+}
 
 // Bytes of the decode kernel's LDS layout for a beam capacity W (carve() in
 // ctcx_decode.hip, same order and alignment).

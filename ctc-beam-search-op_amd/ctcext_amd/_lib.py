@@ -23,6 +23,8 @@ CTCEXT_FLAG_FORCE_LITERAL = 1
 CTCEXT_FLAG_PROFILE = 2
 CTCEXT_FLAG_PHASES = 4
 CTCEXT_FLAG_GLOBAL_STATE = 8   # testing: the global-state tier whatever the shape
+CTCEXT_FLAG_RECORD_RING = 16   # beam records kept in an LDS ring; only the reachable ones written to HBM
+CTCEXT_FLAG_RING_MIN = 32      # testing: the record ring at 8 frames (short items flush); implies RECORD_RING
 CTCEXT_SCORER_BASE = 0
 CTCEXT_SCORER_BIGRAM = 1
 
@@ -68,7 +70,8 @@ class Stats(ctypes.Structure):
                 ("no_label_paths", ctypes.c_int64),
                 ("decode_kernel_ms", ctypes.c_double), ("norm_kernel_ms", ctypes.c_double),
                 ("traceback_ms", ctypes.c_double), ("n_devices", ctypes.c_int32),
-                ("tier", ctypes.c_int32)]
+                ("tier", ctypes.c_int32), ("ring_frames", ctypes.c_int32),
+                ("records_written", ctypes.c_int64)]
 
 
 _lib = None

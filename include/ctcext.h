@@ -51,7 +51,11 @@ enum {
   CTCEXT_FLAG_FORCE_LITERAL = 1,   /* testing: replay every frame through the literal TopN model */
   CTCEXT_FLAG_PROFILE = 2,         /* time the decode kernel with HIP events (ctcext_stats) */
   CTCEXT_FLAG_PHASES = 4,          /* diagnostics: per-item s_memtime phase counters */
-  CTCEXT_FLAG_GLOBAL_STATE = 8     /* testing: decode on the global-state tier whatever the shape */
+  CTCEXT_FLAG_GLOBAL_STATE = 8,    /* testing: decode on the global-state tier whatever the shape */
+  CTCEXT_FLAG_RECORD_RING = 16,    /* keep beam records in an LDS ring and write only those the
+                                      traceback can reach (fewer HBM writes, ~1% more decode time) */
+  CTCEXT_FLAG_RING_MIN = 32        /* testing: the record ring at its smallest (8 frames), so short
+                                      items flush; implies CTCEXT_FLAG_RECORD_RING */
 };
 
 typedef struct ctcext_decoder ctcext_decoder;
@@ -118,6 +122,9 @@ typedef struct {
   int32_t n_devices;               /* devices of the handle */
   int32_t tier;                    /* last decode: 0 the LDS-resident fast tier, 1 the
                                       global-state tier (shapes past the LDS / record limits) */
+  int32_t ring_frames;             /* last decode: frames of the LDS record ring (0: every
+                                      record of every frame written to HBM) */
+  int64_t records_written;         /* last decode: beam records written to HBM (all devices) */
 } ctcext_stats;
 
 /* Handle lifetime.  A handle owns a HIP stream and a grow-only device

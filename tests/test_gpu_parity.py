@@ -134,7 +134,8 @@ def _dup_family(seed, n_want, dtype=np.float32, max_tries=4000):
 
 
 @pytest.mark.parametrize("dtype,flags", [(np.float32, 0), (np.float64, 0),
-                                         (np.float32, _lib.CTCEXT_FLAG_FORCE_LITERAL)])
+                                         (np.float32, _lib.CTCEXT_FLAG_FORCE_LITERAL),
+                                         (np.float32, _lib.CTCEXT_FLAG_RING_MIN)])
 def test_duplicate_entry_state(dtype, flags):
     # the reference's beam holding one BeamEntry twice, reproduced bit-exactly:
     # second roll empties old_cands, second recursion accumulates, shared
@@ -596,3 +597,49 @@ def test_scorer_rejects_positive_scores():
     assert "log-probabilities" in e.value.message
     with pytest.raises(ValueError):
         ctcext_amd.ctc_ext_beam_search_decoder(x, [3], 2, 1, scorer_table=np.zeros((4, 4), np.float32))
+
+
+# ---- the LDS record ring (CTCEXT_FLAG_RECORD_RING, ctcx_decode.hip
+# ring_flush): only the records the traceback can reach are written to HBM,
+# compacted and renumbered.  At its smallest size (8 frames) the random
+# families flush several times per item.
+
+RMIN = _lib.CTCEXT_FLAG_RING_MIN
+
+
+def _stats():
+    return ctcext_amd.get_decoder(0).last_stats
+
+
+def test_record_ring_random_families():
+    _run_random(8101, 80, flags=RMIN, device=True)
+    assert _stats()["ring_frames"] == 8
+    _run_random(8102, 60, flags=RMIN, ties=True)
+    _run_random(8103, 40, flags=RMIN, neg_inf=True)
+    _run_random(8104, 30, flags=RMIN, dtype=np.float64)
+    _run_random(8105, 15, flags=RMIN, T_max=40, B_max=2, C_min=65, C_max=300, W_max=100)
+    _run_random(8106, 20, flags=RMIN, T_max=60, W_min=100, W_max=256, C_max=8)
+
+
+def test_record_ring_matches_direct_records():
+    # cfg3's shape at full item length (ragged): the ring (64 frames at W=128:
+    # six items, one per CU) and every record written to HBM give the same
+    # outputs, and the ring writes fewer records
+    rng = np.random.default_rng(77)
+    T, B, C, W, P = 1500, 6, 29, 128, 3
+    x = rng.standard_normal((T, B, C)).astype(np.float32)
+    sl = np.array([1500, 1499, 33, 8, 1, 1200], np.int32)
+    kw = dict(merge_repeated=True)
+    a, err = _gpu_or_error(x, sl, W, P, kw, device=True, flags=_lib.CTCEXT_FLAG_RECORD_RING)
+    assert err is None, err
+    st = dict(_stats())
+    b, err = _gpu_or_error(x, sl, W, P, kw, device=True)
+    assert err is None, err
+    assert st["ring_frames"] == 64 and _stats()["ring_frames"] == 0
+    full = _stats()["records_written"]
+    assert 0 < st["records_written"] < full, (st["records_written"], full)
+    for p in range(P):
+        for name in ("decoded_indices", "decoded_values", "decoded_shape",
+                     "alignment_indices", "alignment_values", "alignment_shape"):
+            np.testing.assert_array_equal(to_numpy(getattr(a, name)[p]), to_numpy(getattr(b, name)[p]))
+    np.testing.assert_array_equal(to_numpy(a.log_probability), to_numpy(b.log_probability))
