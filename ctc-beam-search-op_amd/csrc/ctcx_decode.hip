@@ -1063,20 +1063,18 @@ __device__ __forceinline__ int heap_events_f32(float s, int c, int sl, unsigned 
       "s_cbranch_scc1 .Lev_evb_%=\n"
       ".Lev_slot_%=:\n\t"
       "v_cmp_eq_u32_e64 s[90:91], %[fs], %[my]\n\t"        // an entry accepted in this chunk is the evicted front
-      "s_lshl_b64 vcc, 1, %[k]\n\t"
-      "v_mov_b32_e32 v243, s85\n\t"
+      "s_mov_b32 m0, %[k]\n\t"
       "v_cndmask_b32_e64 %[my], %[my], -1, s[90:91]\n\t"
-      "v_cndmask_b32_e32 %[my], %[my], v243, vcc\n\t"      // lane k: its entry's slot
+      "v_writelane_b32 %[my], s85, m0\n\t"                 // lane k: its entry's slot
       "s_branch .Lev_loop_%=\n"
       // the evicted front is a branch's entry: a fresh slot; record the
       // eviction; a live re-offer of that branch is now wanted
       ".Lev_evb_%=:\n\t"
       "s_mov_b32 s85, %[nfree]\n\t"
       "s_add_u32 %[nfree], %[nfree], 1\n\t"
-      "s_lshl_b64 s[90:91], 1, %[nv]\n\t"
-      "v_mov_b32_e32 v243, %[fs]\n\t"
+      "s_mov_b32 m0, %[nv]\n\t"
       "s_add_u32 %[nv], %[nv], 1\n\t"
-      "v_cndmask_b32_e64 %[evr], %[evr], v243, s[90:91]\n\t"
+      "v_writelane_b32 %[evr], %[fs], m0\n\t"
       "v_cmp_eq_u32_e64 s[90:91], %[fs], %[c]\n\t"
       "s_and_b64 s[90:91], s[90:91], %[lb]\n\t"
       "s_or_b64 %[rb], %[rb], s[90:91]\n\t"
@@ -1089,7 +1087,7 @@ __device__ __forceinline__ int heap_events_f32(float s, int c, int sl, unsigned 
         [fv] "+s"(fv), [fs] "+s"(fs), [nfree] "+s"(nfree), [nv] "+s"(nv), [k] "=&s"(k), [st] "=&s"(st), [cnt] "+s"(cnt)
       : [s] "v"(s), [c] "v"(c), [sl] "v"(sl), [anc] "v"(anc), [req] "v"(req), [aj] "v"(aj), [al] "v"(al),
         [ar] "v"(ar), [dum] "v"(dum), [lb] "s"(LB), [nb] "s"(nb), [k31] "s"(k31), [khi] "s"(khi)
-      : "memory", "vcc", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96",
+      : "memory", "vcc", "m0", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96",
         "s97", "s98", "s99", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239", "v240", "v241",
         "v242", "v243");
   return st;
@@ -1201,18 +1199,16 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
       "s_cbranch_scc1 .Lem_evb_%=\n"
       ".Lem_slot_%=:\n\t"
       "v_cmp_eq_u32_e64 s[90:91], %[fs], %[my]\n\t"        // an entry accepted in this chunk is the evicted front
-      "s_lshl_b64 vcc, 1, %[k]\n\t"
-      "v_mov_b32_e32 v243, s85\n\t"
+      "s_mov_b32 m0, %[k]\n\t"
       "v_cndmask_b32_e64 %[my], %[my], -1, s[90:91]\n\t"
-      "v_cndmask_b32_e32 %[my], %[my], v243, vcc\n\t"      // lane k: its entry's slot
+      "v_writelane_b32 %[my], s85, m0\n\t"                 // lane k: its entry's slot
       "s_branch .Lem_loop_%=\n"
       ".Lem_evb_%=:\n\t"
       "s_mov_b32 s85, %[nfree]\n\t"
       "s_add_u32 %[nfree], %[nfree], 1\n\t"
-      "s_lshl_b64 s[90:91], 1, %[nv]\n\t"
-      "v_mov_b32_e32 v243, %[fs]\n\t"
+      "s_mov_b32 m0, %[nv]\n\t"
       "s_add_u32 %[nv], %[nv], 1\n\t"
-      "v_cndmask_b32_e64 %[evr], %[evr], v243, s[90:91]\n\t"
+      "v_writelane_b32 %[evr], %[fs], m0\n\t"
       "v_cmp_eq_u32_e64 s[90:91], %[fs], %[c]\n\t"
       "s_and_b64 s[90:91], s[90:91], %[lb]\n\t"
       "s_or_b64 %[rb], %[rb], s[90:91]\n\t"
@@ -1227,7 +1223,7 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
       : [s] "v"(s), [c] "v"(c), [sl] "v"(sl), [anc] "v"(anc), [req] "v"(req), [an1l] "v"(an1l), [an1h] "v"(an1h),
         [rq1l] "v"(rq1l), [rq1h] "v"(rq1h), [aj] "v"(aj), [al] "v"(al), [ar] "v"(ar), [aj1] "v"(aj1),
         [al1] "v"(al1), [ar1] "v"(ar1), [dum] "v"(dum), [lb] "s"(LB), [nb] "s"(nb), [k63] "s"(k63)
-      : "memory", "vcc", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96",
+      : "memory", "vcc", "m0", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96",
         "s97", "s98", "s99", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239", "v240", "v241",
         "v242", "v243", "v244", "v245", "v246", "v247", "v248", "v249", "v250", "v251", "v252", "v253");
   return st;
@@ -1307,19 +1303,18 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
       ".Lew_slot_%=:\n\t"                                                                                    \
       "v_cmp_eq_u32_e64 s[90:91], %[fs], %[my]\n\t"                                                          \
       "v_cmp_eq_u32_e64 s[86:87], %[fs], %[myo]\n\t"                                                         \
-      "s_lshl_b64 vcc, 1, %[k]\n\t"                                                                          \
-      "v_mov_b32_e32 v243, s85\n\t"                                                                          \
+      "s_mov_b32 m0, %[k]\n\t"                                                                               \
+      "s_nop 0\n\t"                                                                                          \
       "v_cndmask_b32_e64 %[my], %[my], -1, s[90:91]\n\t"                                                     \
       "v_cndmask_b32_e64 %[myo], %[myo], -1, s[86:87]\n\t"                                                   \
-      "v_cndmask_b32_e32 %[my], %[my], v243, vcc\n\t"                                                        \
+      "v_writelane_b32 %[my], s85, m0\n\t"                                                                   \
       "s_branch .Lew_loop_%=\n"                                                                              \
       ".Lew_evb_%=:\n\t"                                                                                     \
       "s_mov_b32 s85, %[nfree]\n\t"                                                                          \
       "s_add_u32 %[nfree], %[nfree], 1\n\t"                                                                  \
-      "s_lshl_b64 s[90:91], 1, %[nv]\n\t"                                                                    \
-      "v_mov_b32_e32 v243, %[fs]\n\t"                                                                        \
+      "s_mov_b32 m0, %[nv]\n\t"                                                                              \
       "s_add_u32 %[nv], %[nv], 1\n\t"                                                                        \
-      "v_cndmask_b32_e64 %[evr], %[evr], v243, s[90:91]\n\t"                                                 \
+      "v_writelane_b32 %[evr], %[fs], m0\n\t"                                                                \
       "v_cmp_eq_u32_e64 s[90:91], %[fs], %[c]\n\t"                                                           \
       "s_and_b64 s[90:91], s[90:91], %[lb]\n\t"                                                              \
       "s_or_b64 %[rb], %[rb], s[90:91]\n\t" EVB_OTHER                                                        \
@@ -1335,8 +1330,8 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
         [aj] "v"(aj), [al] "v"(al), [ar] "v"(ar), [dum] "v"(dum), [lb] "s"(LB), [lbo] "s"(LBo), [nb] "s"(nb), \
         [hoff] "s"(hoff), [k31] "s"(k31), [khi] "s"(khi)                                                     \
       : "memory", "vcc", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95",  \
-        "s96", "s97", "s98", "s99", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239", "v240",   \
-        "v241", "v242", "v243", "v244")
+        "s96", "s97", "s98", "s99", "m0", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239",     \
+        "v240", "v241", "v242", "v243", "v244")
 
 template <bool OTHER>
 __device__ __forceinline__ int heap_events2_f32(float s, int c, int sl, int co, int slo, unsigned anc, unsigned req,
@@ -1380,19 +1375,17 @@ __device__ __forceinline__ void extract_f32(unsigned heb, int hi, int lo, int ba
       "s_mov_b64 s[90:91], 1\n\t"                          // lane 0
       "v_mov_b32_e32 v242, 0x7f800000\n\t"                 // the sentinel (+inf, -1)
       "v_mov_b32_e32 v243, -1\n"
+      "s_lshl_b32 s85, s84, 3\n\t"
+      "s_add_u32 s85, s85, %[heb]\n\t"
+      "v_mov_b32_e32 v236, s85\n\t"                      // he[len]: position len - 1 (-8 B per pop)
+      "s_sub_u32 s86, s84, 1\n\t"
+      "s_sub_u32 m0, s86, %[base]\n\t"                    // its lane in srt (-1 per pop)
       ".Lx_top_%=:\n\t"
       "s_cmp_le_i32 s84, %[lo]\n\t"
       "s_cbranch_scc1 .Lx_end_%=\n\t"
-      "s_lshl_b32 s85, s84, 3\n\t"
-      "s_add_u32 s85, s85, %[heb]\n\t"                     // he[len]: position len - 1
-      "s_sub_u32 s86, s84, 1\n\t"
-      "s_sub_u32 s86, s86, %[base]\n\t"
-      "s_lshl_b64 s[88:89], 1, s86\n\t"                    // its lane in srt
-      "v_mov_b32_e32 v236, s85\n\t"
-      "v_mov_b32_e32 v240, %[fs]\n\t"
       "ds_read_b64 v[238:239], v236\n\t"                   // e[len - 1] (every lane: broadcast)
       "v_cndmask_b32_e64 v241, %[dum], v236, s[90:91]\n\t"
-      "v_cndmask_b32_e64 %[srt], %[srt], v240, s[88:89]\n\t"   // the front: position len - 1
+      "v_writelane_b32 %[srt], %[fs], m0\n\t"              // the front: position len - 1
       "ds_write_b64 v241, v[242:243]\n\t"                  // lane 0: the sentinel
       "ds_read_b128 v[232:235], %[al]\n\t"                 // child pairs
       "s_waitcnt lgkmcnt(0)\n\t"
@@ -1425,13 +1418,15 @@ __device__ __forceinline__ void extract_f32(unsigned heb, int hi, int lo, int ba
       "s_cselect_b32 %[fs], s87, s86\n\t"
       "ds_write2_b32 v250, v244, v245 offset1:1\n\t"
       "s_sub_u32 s84, s84, 1\n\t"
+      "s_sub_u32 m0, m0, 1\n\t"
+      "v_subrev_u32_e32 v236, 8, v236\n\t"
       "s_branch .Lx_top_%=\n"
       ".Lx_end_%=:\n\t"
       "s_waitcnt lgkmcnt(0)"
       : [srt] "+v"(srt), [fs] "+s"(fs)
       : [heb] "s"(heb), [hi] "s"(hi), [lo] "s"(lo), [base] "s"(base), [anc] "v"(anc), [req] "v"(req), [aj] "v"(aj),
         [al] "v"(al), [ar] "v"(ar), [dum] "v"(dum), [k31] "s"(k31), [khi] "s"(khi)
-      : "memory", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97",
+      : "memory", "m0", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97",
         "s98", "s99", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239", "v240", "v241", "v242",
         "v243", "v244", "v245", "v246", "v247", "v248", "v249", "v250", "v251");
 }
@@ -1457,19 +1452,17 @@ __device__ __forceinline__ void extract_m2_f32(unsigned heb, int hi, int lo, int
       "s_mov_b64 s[90:91], 1\n\t"                          // lane 0
       "v_mov_b32_e32 v242, 0x7f800000\n\t"                 // the sentinel (+inf, -1)
       "v_mov_b32_e32 v243, -1\n"
+      "s_lshl_b32 s85, s84, 3\n\t"
+      "s_add_u32 s85, s85, %[heb]\n\t"
+      "v_mov_b32_e32 v236, s85\n\t"                      // he[len]: position len - 1 (-8 B per pop)
+      "s_sub_u32 s86, s84, 1\n\t"
+      "s_sub_u32 m0, s86, %[base]\n\t"                    // its lane in srt (-1 per pop)
       ".Ly_top_%=:\n\t"
       "s_cmp_le_i32 s84, %[lo]\n\t"
       "s_cbranch_scc1 .Ly_end_%=\n\t"
-      "s_lshl_b32 s85, s84, 3\n\t"
-      "s_add_u32 s85, s85, %[heb]\n\t"                     // he[len]: position len - 1
-      "s_sub_u32 s86, s84, 1\n\t"
-      "s_sub_u32 s86, s86, %[base]\n\t"
-      "s_lshl_b64 s[88:89], 1, s86\n\t"                    // its lane in srt
-      "v_mov_b32_e32 v236, s85\n\t"
-      "v_mov_b32_e32 v240, %[fs]\n\t"
       "ds_read_b64 v[238:239], v236\n\t"                   // e[len - 1] (every lane: broadcast)
       "v_cndmask_b32_e64 v241, %[dum], v236, s[90:91]\n\t"
-      "v_cndmask_b32_e64 %[srt], %[srt], v240, s[88:89]\n\t"   // the front: position len - 1
+      "v_writelane_b32 %[srt], %[fs], m0\n\t"              // the front: position len - 1
       "ds_write_b64 v241, v[242:243]\n\t"                  // lane 0: the sentinel
       "ds_read_b128 v[232:235], %[al]\n\t"                 // group 0 child pairs
       "ds_read_b128 v[252:255], %[al] offset:1024\n\t"     // group 1 child pairs
@@ -1521,6 +1514,8 @@ __device__ __forceinline__ void extract_m2_f32(unsigned heb, int hi, int lo, int
       "s_bitcmp1_b32 s96, 0\n\t"                           // keep: v stays at the root
       "s_cselect_b32 %[fs], s87, s86\n\t"
       "s_sub_u32 s84, s84, 1\n\t"
+      "s_sub_u32 m0, m0, 1\n\t"
+      "v_subrev_u32_e32 v236, 8, v236\n\t"
       "s_branch .Ly_top_%=\n"
       ".Ly_end_%=:\n\t"
       "s_waitcnt lgkmcnt(0)"
@@ -1529,7 +1524,7 @@ __device__ __forceinline__ void extract_m2_f32(unsigned heb, int hi, int lo, int
       : [heb] "s"(heb), [hi] "s"(hi), [lo] "s"(lo), [base] "s"(base), [anc] "v"(anc), [req] "v"(req),
         [an1l] "v"(an1l), [an1h] "v"(an1h), [rq1l] "v"(rq1l), [rq1h] "v"(rq1h), [aj] "v"(aj), [al] "v"(al),
         [ar] "v"(ar), [aj1] "v"(aj1), [al1] "v"(al1), [ar1] "v"(ar1), [dum] "v"(dum), [k63] "s"(k63)
-      : "memory", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97",
+      : "memory", "m0", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97",
         "s98", "s99", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239", "v240", "v241", "v242",
         "v243", "v244", "v245", "v246", "v247", "v248", "v249", "v250", "v251", "v252", "v253", "v254", "v255");
 }
