@@ -1018,9 +1018,8 @@ __device__ __forceinline__ int heap_events_f32(float s, int c, int sl, unsigned 
       "v_mov_b32_e32 v241, s85\n\t"
       "v_cndmask_b32_e64 v237, v232, v234, s[92:93]\n\t"   // cv
       "v_cndmask_b32_e64 v238, v233, v235, s[92:93]\n\t"   // cs
-      "v_xor_b32_e32 v239, s92, %[req]\n\t"
+      "v_bitop3_b32 v239, s92, %[req], %[anc] bitop3:0x28\n\t"
       "v_cmp_lt_f32_e64 s[96:97], s84, v237\n\t"           // gt: min child > v
-      "v_and_b32_e32 v239, v239, %[anc]\n\t"
       "v_readfirstlane_b32 s86, v237\n\t"                  // c0: the root's min child
       "v_cmp_eq_u32_e64 s[94:95], 0, v239\n\t"             // onp: on the root's min-child path
       "v_readfirstlane_b32 s87, v238\n\t"
@@ -1136,16 +1135,13 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
       "v_mov_b32_e32 v241, s85\n\t"
       "v_cndmask_b32_e64 v237, v232, v234, s[92:93]\n\t"   // cv0
       "v_cndmask_b32_e64 v238, v233, v235, s[92:93]\n\t"   // cs0
-      "v_xor_b32_e32 v239, s92, %[req]\n\t"
+      "v_bitop3_b32 v239, s92, %[req], %[anc] bitop3:0x28\n\t"
       "v_cmp_lt_f32_e64 s[96:97], s84, v237\n\t"           // gt0
-      "v_and_b32_e32 v239, v239, %[anc]\n\t"
       "v_readfirstlane_b32 s86, v237\n\t"                  // c0: the root's min child
       "v_cmp_eq_u32_e64 s[94:95], 0, v239\n\t"             // onp0
       "v_readfirstlane_b32 s87, v238\n\t"
-      "v_xor_b32_e32 v248, s92, %[rq1l]\n\t"
-      "v_xor_b32_e32 v249, s93, %[rq1h]\n\t"
-      "v_and_b32_e32 v248, v248, %[an1l]\n\t"
-      "v_and_b32_e32 v249, v249, %[an1h]\n\t"
+      "v_bitop3_b32 v248, s92, %[rq1l], %[an1l] bitop3:0x28\n\t"
+      "v_bitop3_b32 v249, s93, %[rq1h], %[an1h] bitop3:0x28\n\t"
       "v_or_b32_e32 v248, v248, v249\n\t"
       "v_cndmask_b32_e64 v250, v244, v246, %[p1]\n\t"      // cv1
       "v_cndmask_b32_e64 v251, v245, v247, %[p1]\n\t"      // cs1
@@ -1239,26 +1235,37 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
 #define CTCX_HEV2_ASM(EVB_OTHER, BAT_OTHER)                                                                   \
   asm volatile(                                                                                              \
       "s_mov_b32 %[st], 0\n\t"                                                                               \
+      "s_not_b64 s[80:81], %[done]\n\t"                     /* lanes still to come */                        \
       "v_cmp_lt_f32_e64 s[88:89], %[fv], %[s]\n\t"                                                           \
       "s_and_b64 s[88:89], s[88:89], %[nc]\n\t"                                                              \
       "s_or_b64 s[88:89], s[88:89], %[rb]\n\t"                                                               \
-      "s_andn2_b64 s[88:89], s[88:89], %[done]\n\t"                                                          \
+      "s_and_b64 s[88:89], s[88:89], s[80:81]\n\t"                                                           \
       "s_cbranch_scc0 .Lew_exit_%=\n\t"                                                                      \
       "s_ff1_i32_b64 %[k], s[88:89]\n\t"                                                                     \
       "s_bitcmp1_b64 %[lb], %[k]\n\t"                                                                        \
       "s_cbranch_scc1 .Lew_rare_%=\n\t"                                                                      \
-      "ds_read_b128 v[232:235], %[al]\n\t"                                                                   \
-      "s_branch .Lew_tail_%=\n"                                                                              \
-      ".Lew_loop_%=:\n\t" CTCX_EVCNT                                                                         \
+      "ds_read_b128 v[232:235], %[al]\n"                                                                     \
+      ".Lew_tail_%=:\n\t"                                                                                    \
+      "s_lshl_b64 s[80:81], -2, %[k]\n\t"                   /* lanes after k */                              \
+      "v_readlane_b32 s84, %[s], %[k]\n\t"                                                                   \
+      "s_mov_b32 s85, %[fs]\n\t"                                                                             \
+      "s_cmp_lt_i32 %[fs], %[nb]\n\t"                                                                        \
+      "s_cbranch_scc1 .Lew_evb_%=\n"                                                                         \
+      ".Lew_slot_%=:\n\t"                                                                                    \
+      "v_cmp_eq_u32_e64 s[90:91], %[fs], %[my]\n\t"                                                          \
+      "v_cmp_eq_u32_e64 s[86:87], %[fs], %[myo]\n\t"                                                         \
+      "s_mov_b32 m0, %[k]\n\t"                                                                               \
+      "v_cndmask_b32_e64 %[my], %[my], -1, s[90:91]\n\t"                                                     \
+      "v_cndmask_b32_e64 %[myo], %[myo], -1, s[86:87]\n\t"                                                   \
+      "v_writelane_b32 %[my], s85, m0\n\t" CTCX_EVCNT                                                        \
       "s_waitcnt lgkmcnt(0)\n\t"                                                                             \
       "v_cmp_ngt_f32_e64 s[92:93], v234, v232\n\t"                                                           \
       "v_mov_b32_e32 v240, s84\n\t"                                                                          \
       "v_mov_b32_e32 v241, s85\n\t"                                                                          \
       "v_cndmask_b32_e64 v237, v232, v234, s[92:93]\n\t"                                                     \
       "v_cndmask_b32_e64 v238, v233, v235, s[92:93]\n\t"                                                     \
-      "v_xor_b32_e32 v239, s92, %[req]\n\t"                                                                  \
+      "v_bitop3_b32 v239, s92, %[req], %[anc] bitop3:0x28\n\t"   /* (pickR ^ req) & anc */                 \
       "v_cmp_lt_f32_e64 s[96:97], s84, v237\n\t"                                                             \
-      "v_and_b32_e32 v239, v239, %[anc]\n\t"                                                                 \
       "v_readfirstlane_b32 s86, v237\n\t"                                                                    \
       "v_cmp_eq_u32_e64 s[94:95], 0, v239\n\t"                                                               \
       "v_readfirstlane_b32 s87, v238\n\t"                                                                    \
@@ -1268,8 +1275,7 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
       "s_cselect_b32 %[fv], s84, s86\n\t"                                                                    \
       "s_cselect_b32 %[fs], s85, s87\n\t"                                                                    \
       "s_or_b64 s[98:99], s[98:99], s[96:97]\n\t"                                                            \
-      "s_add_u32 s85, %[k], %[hoff]\n\t"                                                                     \
-      "v_cmp_lt_i32_e64 vcc, s85, %[sl]\n\t"                                                                 \
+      "v_cmp_lt_i32_e64 vcc, %[k], %[sl]\n\t"                                                                \
       "v_cmp_lt_f32_e64 s[88:89], %[fv], %[s]\n\t"                                                           \
       "s_and_b64 s[90:91], s[94:95], s[98:99]\n\t"                                                           \
       "s_ff1_i32_b64 s86, s[90:91]\n\t"                                                                      \
@@ -1288,27 +1294,12 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
       "s_or_b64 s[88:89], s[88:89], %[rb]\n\t"                                                               \
       "ds_write2_b32 v236, v240, v241 offset1:1\n\t"                                                         \
       "ds_read_b128 v[232:235], %[al]\n\t"                                                                   \
-      "s_andn2_b64 s[88:89], s[88:89], %[done]\n\t"                                                          \
+      "s_and_b64 s[88:89], s[88:89], s[80:81]\n\t"                                                           \
       "s_cbranch_scc0 .Lew_exit_%=\n\t"                                                                      \
       "s_ff1_i32_b64 %[k], s[88:89]\n\t"                                                                     \
       "s_bitcmp1_b64 %[lb], %[k]\n\t"                                                                        \
-      "s_cbranch_scc1 .Lew_rare_%=\n"                                                                        \
-      ".Lew_tail_%=:\n\t"                                                                                    \
-      "s_lshl_b64 s[90:91], -2, %[k]\n\t"                                                                    \
-      "s_not_b64 %[done], s[90:91]\n\t"                                                                      \
-      "v_readlane_b32 s84, %[s], %[k]\n\t"                                                                   \
-      "s_mov_b32 s85, %[fs]\n\t"                                                                             \
-      "s_cmp_lt_i32 %[fs], %[nb]\n\t"                                                                        \
-      "s_cbranch_scc1 .Lew_evb_%=\n"                                                                         \
-      ".Lew_slot_%=:\n\t"                                                                                    \
-      "v_cmp_eq_u32_e64 s[90:91], %[fs], %[my]\n\t"                                                          \
-      "v_cmp_eq_u32_e64 s[86:87], %[fs], %[myo]\n\t"                                                         \
-      "s_mov_b32 m0, %[k]\n\t"                                                                               \
-      "s_nop 0\n\t"                                                                                          \
-      "v_cndmask_b32_e64 %[my], %[my], -1, s[90:91]\n\t"                                                     \
-      "v_cndmask_b32_e64 %[myo], %[myo], -1, s[86:87]\n\t"                                                   \
-      "v_writelane_b32 %[my], s85, m0\n\t"                                                                   \
-      "s_branch .Lew_loop_%=\n"                                                                              \
+      "s_cbranch_scc0 .Lew_tail_%=\n\t"                     /* the next push, unless k is rare */            \
+      "s_branch .Lew_rare_%=\n"                                                                              \
       ".Lew_evb_%=:\n\t"                                                                                     \
       "s_mov_b32 s85, %[nfree]\n\t"                                                                          \
       "s_add_u32 %[nfree], %[nfree], 1\n\t"                                                                  \
@@ -1322,16 +1313,17 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
       ".Lew_rare_%=:\n\t"                                                                                    \
       "s_mov_b32 %[st], 1\n"                                                                                 \
       ".Lew_exit_%=:\n\t"                                                                                    \
+      "s_not_b64 %[done], s[80:81]\n\t"                                                                      \
       "s_waitcnt lgkmcnt(0)"                                                                                 \
       : [my] "+v"(myslot), [myo] "+v"(myo), [evr] "+v"(evr), [bat] "+v"(bat), [bato] "+v"(bato),            \
         [nc] "+s"(NC), [rb] "+s"(RB), [rbo] "+s"(RBo), [done] "+s"(done), [fv] "+s"(fv), [fs] "+s"(fs),     \
         [nfree] "+s"(nfree), [nv] "+s"(nv), [k] "=&s"(k), [st] "=&s"(st), [cnt] "+s"(cnt)                    \
       : [s] "v"(s), [c] "v"(c), [sl] "v"(sl), [co] "v"(co), [slo] "v"(slo), [anc] "v"(anc), [req] "v"(req),  \
         [aj] "v"(aj), [al] "v"(al), [ar] "v"(ar), [dum] "v"(dum), [lb] "s"(LB), [lbo] "s"(LBo), [nb] "s"(nb), \
-        [hoff] "s"(hoff), [k31] "s"(k31), [khi] "s"(khi)                                                     \
-      : "memory", "vcc", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95",  \
-        "s96", "s97", "s98", "s99", "m0", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239",     \
-        "v240", "v241", "v242", "v243", "v244")
+        [k31] "s"(k31), [khi] "s"(khi)                                                                       \
+      : "memory", "vcc", "s80", "s81", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93",  \
+        "s94", "s95", "s96", "s97", "s98", "s99", "m0", "v232", "v233", "v234", "v235", "v236", "v237",       \
+        "v238", "v239", "v240", "v241", "v242", "v243", "v244")
 
 template <bool OTHER>
 __device__ __forceinline__ int heap_events2_f32(float s, int c, int sl, int co, int slo, unsigned anc, unsigned req,
@@ -1344,12 +1336,13 @@ __device__ __forceinline__ int heap_events2_f32(float s, int c, int sl, int co, 
   const uint64_t k31 = 0x80000000ull, khi = 0xffffffff00000000ull;
   // every scalar operand provably uniform (the asm's "s" constraints)
   NC = uni64(NC); RB = uni64(RB); RBo = uni64(RBo); done = uni64(done); LB = uni64(LB); LBo = uni64(LBo);
-  fv = uni(fv); fs = uni(fs); nfree = uni(nfree); nv = uni(nv); nb = uni(nb); hoff = uni(hoff); cnt = uni(cnt);
+  fv = uni(fv); fs = uni(fs); nfree = uni(nfree); nv = uni(nv); nb = uni(nb); cnt = uni(cnt);
+  (void)hoff;   // sl / slo arrive relative to the half (turn start - hoff)
   if constexpr (OTHER)
     CTCX_HEV2_ASM("v_cmp_eq_u32_e64 s[90:91], %[fs], %[co]\n\t"
                   "s_and_b64 s[90:91], s[90:91], %[lbo]\n\t"
                   "s_or_b64 %[rbo], %[rbo], s[90:91]\n\t",
-                  "v_cmp_lt_i32_e64 s[86:87], s85, %[slo]\n\t"
+                  "v_cmp_lt_i32_e64 s[86:87], %[k], %[slo]\n\t"
                   "v_mov_b32_e32 v244, %[fv]\n\t"
                   "s_nop 1\n\t"
                   "v_cndmask_b32_e64 %[bato], %[bato], v244, s[86:87]\n\t");
@@ -1394,9 +1387,8 @@ __device__ __forceinline__ void extract_f32(unsigned heb, int hi, int lo, int ba
       "v_mov_b32_e32 v245, v239\n\t"
       "v_cndmask_b32_e64 v248, v232, v234, s[92:93]\n\t"   // cv
       "v_cndmask_b32_e64 v249, v233, v235, s[92:93]\n\t"   // cs
-      "v_xor_b32_e32 v251, s92, %[req]\n\t"
+      "v_bitop3_b32 v251, s92, %[req], %[anc] bitop3:0x28\n\t"
       "v_cmp_lt_f32_e64 s[96:97], v238, v248\n\t"          // gt: min child > v
-      "v_and_b32_e32 v251, v251, %[anc]\n\t"
       "v_readfirstlane_b32 s87, v239\n\t"                  // v's slot
       "v_cmp_eq_u32_e64 s[94:95], 0, v251\n\t"             // onp
       "v_readfirstlane_b32 s86, v249\n\t"                  // s0
@@ -1473,16 +1465,13 @@ __device__ __forceinline__ void extract_m2_f32(unsigned heb, int hi, int lo, int
       "v_mov_b32_e32 v245, v239\n\t"
       "v_cndmask_b32_e64 v248, v232, v234, s[92:93]\n\t"   // cv0
       "v_cndmask_b32_e64 v249, v233, v235, s[92:93]\n\t"   // cs0
-      "v_xor_b32_e32 v251, s92, %[req]\n\t"
+      "v_bitop3_b32 v251, s92, %[req], %[anc] bitop3:0x28\n\t"
       "v_cmp_lt_f32_e64 s[96:97], v238, v248\n\t"          // gt0: min child > v
-      "v_and_b32_e32 v251, v251, %[anc]\n\t"
       "v_readfirstlane_b32 s87, v239\n\t"                  // v's slot
       "v_cmp_eq_u32_e64 s[94:95], 0, v251\n\t"             // onp0
       "v_readfirstlane_b32 s86, v249\n\t"                  // s0
-      "v_xor_b32_e32 %[t0], s92, %[rq1l]\n\t"
-      "v_xor_b32_e32 %[t1], s93, %[rq1h]\n\t"
-      "v_and_b32_e32 %[t0], %[t0], %[an1l]\n\t"
-      "v_and_b32_e32 %[t1], %[t1], %[an1h]\n\t"
+      "v_bitop3_b32 %[t0], s92, %[rq1l], %[an1l] bitop3:0x28\n\t"
+      "v_bitop3_b32 %[t1], s93, %[rq1h], %[an1h] bitop3:0x28\n\t"
       "v_or_b32_e32 %[t0], %[t0], %[t1]\n\t"
       "v_cndmask_b32_e64 %[c1v], v252, v254, %[p1]\n\t"    // cv1
       "v_cndmask_b32_e64 %[c1s], v253, v255, %[p1]\n\t"    // cs1
@@ -1827,7 +1816,8 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
           int k, cnt = 0;                                                                                         \
           fv = uni(fv); fs = uni(fs); nfree = uni(nfree); nv = uni(nv);                                           \
           const uint64_t ta = pc ? __builtin_amdgcn_s_memtime() : 0;                                              \
-          const int est = heap_events2_f32<H == 0>(sw[H], cw[H], slw[H], cw[O], slw[O], geo.anc, geo.req, aj,   \
+          const int est = heap_events2_f32<H == 0>(sw[H], cw[H], slw[H] - 64 * H, cw[O], slw[O] - 64 * H,      \
+                                                   geo.anc, geo.req, aj,                                         \
                                                    al, ar, dum, mys[H], mys[O], evr, batw[H], batw[O], NCw[H],   \
                                                    RBw[H], RBw[O], donew[H], LBw[H], LBw[O], fv, fs, nfree, nv,  \
                                                    uni(nb), 64 * H, k, cnt);                                     \
