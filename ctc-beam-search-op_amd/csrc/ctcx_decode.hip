@@ -1232,9 +1232,10 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
 // (OTHER) a branch eviction makes the second half's re-offer of it wanted (rbo)
 // and its turns still to start see every new front (bato).  sl is
 // window-relative (0..127); hoff is the half's first window position.
-#define CTCX_HEV2_ASM(EVB_OTHER, BAT_OTHER)                                                                   \
+#define CTCX_HEV2_ASM(EVB_OTHER, BAT_OTHER, MYO_CMP, MYO_SET)                                                \
   asm volatile(                                                                                              \
       "s_mov_b32 %[st], 0\n\t"                                                                               \
+      "s_mov_b32 s99, -1\n\t"                              /* cnd's high word: lanes 32..63 always stop */   \
       "s_not_b64 s[80:81], %[done]\n\t"                     /* lanes still to come */                        \
       "v_cmp_lt_f32_e64 s[88:89], %[fv], %[s]\n\t"                                                           \
       "s_and_b64 s[88:89], s[88:89], %[nc]\n\t"                                                              \
@@ -1252,11 +1253,9 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
       "s_cmp_lt_i32 %[fs], %[nb]\n\t"                                                                        \
       "s_cbranch_scc1 .Lew_evb_%=\n"                                                                         \
       ".Lew_slot_%=:\n\t"                                                                                    \
-      "v_cmp_eq_u32_e64 s[90:91], %[fs], %[my]\n\t"                                                          \
-      "v_cmp_eq_u32_e64 s[86:87], %[fs], %[myo]\n\t"                                                         \
+      "v_cmp_eq_u32_e64 s[90:91], %[fs], %[my]\n\t" MYO_CMP                                                  \
       "s_mov_b32 m0, %[k]\n\t"                                                                               \
-      "v_cndmask_b32_e64 %[my], %[my], -1, s[90:91]\n\t"                                                     \
-      "v_cndmask_b32_e64 %[myo], %[myo], -1, s[86:87]\n\t"                                                   \
+      "v_cndmask_b32_e64 %[my], %[my], -1, s[90:91]\n\t" MYO_SET                                             \
       "v_writelane_b32 %[my], s85, m0\n\t" CTCX_EVCNT                                                        \
       "s_waitcnt lgkmcnt(0)\n\t"                                                                             \
       "v_cmp_ngt_f32_e64 s[92:93], v234, v232\n\t"                                                           \
@@ -1269,12 +1268,11 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
       "v_readfirstlane_b32 s86, v237\n\t"                                                                    \
       "v_cmp_eq_u32_e64 s[94:95], 0, v239\n\t"                                                               \
       "v_readfirstlane_b32 s87, v238\n\t"                                                                    \
-      "s_and_b64 s[98:99], s[92:93], %[k31]\n\t"                                                             \
-      "s_or_b64 s[98:99], s[98:99], %[khi]\n\t"                                                              \
+      "s_and_b32 s98, s92, %[k31]\n\t"                                                                       \
       "s_bitcmp1_b32 s96, 0\n\t"                                                                             \
       "s_cselect_b32 %[fv], s84, s86\n\t"                                                                    \
       "s_cselect_b32 %[fs], s85, s87\n\t"                                                                    \
-      "s_or_b64 s[98:99], s[98:99], s[96:97]\n\t"                                                            \
+      "s_or_b32 s98, s98, s96\n\t"                         /* cnd: gt, or a min child that is not a lane */  \
       "v_cmp_lt_i32_e64 vcc, %[k], %[sl]\n\t"                                                                \
       "v_cmp_lt_f32_e64 s[88:89], %[fv], %[s]\n\t"                                                           \
       "s_and_b64 s[90:91], s[94:95], s[98:99]\n\t"                                                           \
@@ -1320,7 +1318,7 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
         [nfree] "+s"(nfree), [nv] "+s"(nv), [k] "=&s"(k), [st] "=&s"(st), [cnt] "+s"(cnt)                    \
       : [s] "v"(s), [c] "v"(c), [sl] "v"(sl), [co] "v"(co), [slo] "v"(slo), [anc] "v"(anc), [req] "v"(req),  \
         [aj] "v"(aj), [al] "v"(al), [ar] "v"(ar), [dum] "v"(dum), [lb] "s"(LB), [lbo] "s"(LBo), [nb] "s"(nb), \
-        [k31] "s"(k31), [khi] "s"(khi)                                                                       \
+        [k31] "s"(k31)                                                                                       \
       : "memory", "vcc", "s80", "s81", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93",  \
         "s94", "s95", "s96", "s97", "s98", "s99", "m0", "v232", "v233", "v234", "v235", "v236", "v237",       \
         "v238", "v239", "v240", "v241", "v242", "v243", "v244")
@@ -1333,7 +1331,7 @@ __device__ __forceinline__ int heap_events2_f32(float s, int c, int sl, int co, 
                                                 uint64_t LBo, float& fv, int& fs, int& nfree, int& nv, int nb,
                                                 int hoff, int& k, int& cnt) {
   int st;
-  const uint64_t k31 = 0x80000000ull, khi = 0xffffffff00000000ull;
+  const unsigned k31 = 0x80000000u;
   // every scalar operand provably uniform (the asm's "s" constraints)
   NC = uni64(NC); RB = uni64(RB); RBo = uni64(RBo); done = uni64(done); LB = uni64(LB); LBo = uni64(LBo);
   fv = uni(fv); fs = uni(fs); nfree = uni(nfree); nv = uni(nv); nb = uni(nb); cnt = uni(cnt);
@@ -1345,9 +1343,11 @@ __device__ __forceinline__ int heap_events2_f32(float s, int c, int sl, int co, 
                   "v_cmp_lt_i32_e64 s[86:87], %[k], %[slo]\n\t"
                   "v_mov_b32_e32 v244, %[fv]\n\t"
                   "s_nop 1\n\t"
-                  "v_cndmask_b32_e64 %[bato], %[bato], v244, s[86:87]\n\t");
+                  "v_cndmask_b32_e64 %[bato], %[bato], v244, s[86:87]\n\t",
+                  "", "");   // the second half has accepted nothing yet: no myo to invalidate
   else
-    CTCX_HEV2_ASM("", "");
+    CTCX_HEV2_ASM("", "", "v_cmp_eq_u32_e64 s[86:87], %[fs], %[myo]\n\t",
+                  "v_cndmask_b32_e64 %[myo], %[myo], -1, s[86:87]\n\t");
   return st;
 }
 
