@@ -1360,22 +1360,23 @@ __device__ __forceinline__ int heap_events2_f32(float s, int c, int sl, int co, 
 // operand registers are rewritten only after the s_waitcnt that retires them.
 __device__ __forceinline__ void extract_f32(unsigned heb, int hi, int lo, int base, unsigned anc, unsigned req,
                                             unsigned aj, unsigned al, unsigned ar, unsigned dum, int& srt, int& fs) {
-  const uint64_t k31 = 0x80000000ull, khi = 0xffffffff00000000ull;
+  const unsigned k31 = 0x80000000u;
   // every scalar operand provably uniform (the asm's "s" constraints)
   heb = (unsigned)uni((int)heb); hi = uni(hi); lo = uni(lo); base = uni(base); fs = uni(fs);
   asm volatile(
       "s_mov_b32 s84, %[hi]\n\t"
-      "s_mov_b64 s[90:91], 1\n\t"                          // lane 0
-      "v_mov_b32_e32 v242, 0x7f800000\n\t"                 // the sentinel (+inf, -1)
-      "v_mov_b32_e32 v243, -1\n"
-      "s_lshl_b32 s85, s84, 3\n\t"
-      "s_add_u32 s85, s85, %[heb]\n\t"
-      "v_mov_b32_e32 v236, s85\n\t"                      // he[len]: position len - 1 (-8 B per pop)
-      "s_sub_u32 s86, s84, 1\n\t"
-      "s_sub_u32 m0, s86, %[base]\n\t"                    // its lane in srt (-1 per pop)
-      ".Lx_top_%=:\n\t"
       "s_cmp_le_i32 s84, %[lo]\n\t"
       "s_cbranch_scc1 .Lx_end_%=\n\t"
+      "s_mov_b64 s[90:91], 1\n\t"                          // lane 0
+      "s_mov_b32 s99, -1\n\t"                              // cnd's high word: lanes 32..63 always stop
+      "v_mov_b32_e32 v242, 0x7f800000\n\t"                 // the sentinel (+inf, -1)
+      "v_mov_b32_e32 v243, -1\n\t"
+      "s_lshl_b32 s85, s84, 3\n\t"
+      "s_add_u32 s85, s85, %[heb]\n\t"
+      "v_mov_b32_e32 v236, s85\n\t"                        // he[len]: position len - 1 (-8 B per pop)
+      "s_sub_u32 s86, s84, 1\n\t"
+      "s_sub_u32 m0, s86, %[base]\n"                       // its lane in srt (-1 per pop)
+      ".Lx_top_%=:\n\t"
       "ds_read_b64 v[238:239], v236\n\t"                   // e[len - 1] (every lane: broadcast)
       "v_cndmask_b32_e64 v241, %[dum], v236, s[90:91]\n\t"
       "v_writelane_b32 %[srt], %[fs], m0\n\t"              // the front: position len - 1
@@ -1383,44 +1384,42 @@ __device__ __forceinline__ void extract_f32(unsigned heb, int hi, int lo, int ba
       "ds_read_b128 v[232:235], %[al]\n\t"                 // child pairs
       "s_waitcnt lgkmcnt(0)\n\t"
       "v_cmp_ngt_f32_e64 s[92:93], v234, v232\n\t"         // pickR
-      "v_mov_b32_e32 v244, v238\n\t"
-      "v_mov_b32_e32 v245, v239\n\t"
+      "v_readfirstlane_b32 s87, v239\n\t"                  // v's slot
+      "v_subrev_u32_e32 v236, 8, v236\n\t"
       "v_cndmask_b32_e64 v248, v232, v234, s[92:93]\n\t"   // cv
       "v_cndmask_b32_e64 v249, v233, v235, s[92:93]\n\t"   // cs
       "v_bitop3_b32 v251, s92, %[req], %[anc] bitop3:0x28\n\t"
       "v_cmp_lt_f32_e64 s[96:97], v238, v248\n\t"          // gt: min child > v
-      "v_readfirstlane_b32 s87, v239\n\t"                  // v's slot
-      "v_cmp_eq_u32_e64 s[94:95], 0, v251\n\t"             // onp
       "v_readfirstlane_b32 s86, v249\n\t"                  // s0
-      "s_and_b64 s[98:99], s[92:93], %[k31]\n\t"
-      "s_or_b64 s[98:99], s[98:99], %[khi]\n\t"
-      "s_or_b64 s[98:99], s[98:99], s[96:97]\n\t"          // cnd
+      "v_cmp_eq_u32_e64 s[94:95], 0, v251\n\t"             // onp
+      "s_and_b32 s98, s92, %[k31]\n\t"
+      "s_or_b32 s98, s98, s96\n\t"                         // cnd (low word)
       "s_and_b64 s[88:89], s[94:95], s[98:99]\n\t"         // cm
       "s_ff1_i32_b64 s88, s[88:89]\n\t"                    // the stop
       "s_lshl_b64 s[88:89], -2, s88\n\t"
       "s_andn2_b64 s[94:95], s[94:95], s[88:89]\n\t"       // live
       "s_andn2_b64 s[88:89], s[94:95], s[96:97]\n\t"       // up
-      "s_and_b64 s[98:99], s[94:95], s[98:99]\n\t"         // the stop
+      "s_and_b64 s[80:81], s[94:95], s[98:99]\n\t"         // the stop
       "v_cndmask_b32_e64 v250, %[al], %[ar], s[92:93]\n\t"
       "v_cndmask_b32_e64 v247, %[dum], %[aj], s[88:89]\n\t"
       "v_cndmask_b32_e64 v250, v250, %[aj], s[96:97]\n\t"
       "ds_write2_b32 v247, v248, v249 offset1:1\n\t"
-      "v_cndmask_b32_e64 v250, %[dum], v250, s[98:99]\n\t"
+      "v_cndmask_b32_e64 v250, %[dum], v250, s[80:81]\n\t"
       "s_bitcmp1_b32 s96, 0\n\t"                           // keep: v stays at the root
       "s_cselect_b32 %[fs], s87, s86\n\t"
-      "ds_write2_b32 v250, v244, v245 offset1:1\n\t"
+      "ds_write2_b32 v250, v238, v239 offset1:1\n\t"
       "s_sub_u32 s84, s84, 1\n\t"
       "s_sub_u32 m0, m0, 1\n\t"
-      "v_subrev_u32_e32 v236, 8, v236\n\t"
-      "s_branch .Lx_top_%=\n"
+      "s_cmp_gt_i32 s84, %[lo]\n\t"
+      "s_cbranch_scc1 .Lx_top_%=\n"
       ".Lx_end_%=:\n\t"
       "s_waitcnt lgkmcnt(0)"
       : [srt] "+v"(srt), [fs] "+s"(fs)
       : [heb] "s"(heb), [hi] "s"(hi), [lo] "s"(lo), [base] "s"(base), [anc] "v"(anc), [req] "v"(req), [aj] "v"(aj),
-        [al] "v"(al), [ar] "v"(ar), [dum] "v"(dum), [k31] "s"(k31), [khi] "s"(khi)
-      : "memory", "m0", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96", "s97",
-        "s98", "s99", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239", "v240", "v241", "v242",
-        "v243", "v244", "v245", "v246", "v247", "v248", "v249", "v250", "v251");
+        [al] "v"(al), [ar] "v"(ar), [dum] "v"(dum), [k31] "s"(k31)
+      : "memory", "m0", "s80", "s81", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94",
+        "s95", "s96", "s97", "s98", "s99", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239", "v240",
+        "v241", "v242", "v243", "v244", "v245", "v246", "v247", "v248", "v249", "v250", "v251");
 }
 
 // extract_f32 over the two-group heap (beams 129..256: the push_m2 sift), for
@@ -1685,6 +1684,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
   // bottom or flagged lane, is skipped whole (what matters at large C).
   const int Cm1 = C - 1;
   const float rcp = 1.0f / (float)Cm1;
+  const int q128 = 128 / Cm1, r128 = 128 - q128 * Cm1;   // a window's 128 offers in (branch, label index)
   int i0 = 0, li0 = 0;   // the chunk's first offer: branch i0, label index li0
   bool stop = false;
   // large C (compacted chunks): the gathered offers, the span's first offer,
@@ -1719,7 +1719,9 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
           wli[h] = wv[h] ? x - q * Cm1 : 0;
           wl[h] = wli[h] + (wli[h] >= blank ? 1 : 0);
         }
-        for (li0 += 128; li0 >= Cm1; li0 -= Cm1) ++i0;
+        i0 += q128;   // 128 offers on: (i0, li0) + (q128, r128), one carry
+        li0 += r128;
+        if (li0 >= Cm1) { li0 -= Cm1; ++i0; }
         int bl[2], bflg[2], bsti[2], hd[2];
         T bt[2], bob[2], bcb[2], bcn[2], xl[2];
         uint64_t blm[2];
