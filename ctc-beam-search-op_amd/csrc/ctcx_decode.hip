@@ -1698,216 +1698,221 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
   while (i0 < nb && !stop) {
     if constexpr (RN == 1 && !BIG && sizeof(T) == 4 && !SC::kStateful) {
       if (st == kTopHeap && W >= 2) {
-        // ---- HEAP_SORTED, C <= 64, float: 128-offer windows (two halves of
-        // 64 lanes).  The same offer semantics as the 64-offer chunk below,
-        // with window positions 0..127 in place of lanes: one batch of reads,
-        // one skip test, one child walk and one flush per window, and the
-        // events of the first half, then the second, in one register state.
-        const uint64_t tc0 = pc ? __builtin_amdgcn_s_memtime() : 0;
-        const bool turnw = (li0 == 0);
-        int wi[2], wli[2], wl[2];
-        bool wv[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int x = li0 + lane + 64 * h;
-          int q = (int)((float)x * rcp);
-          q -= (q * Cm1 > x) ? 1 : 0;
-          q += ((q + 1) * Cm1 <= x) ? 1 : 0;
-          const int iv = i0 + q;
-          wv[h] = iv < nb;
-          wi[h] = wv[h] ? iv : i0;
-          wli[h] = wv[h] ? x - q * Cm1 : 0;
-          wl[h] = wli[h] + (wli[h] >= blank ? 1 : 0);
-        }
-        i0 += q128;   // 128 offers on: (i0, li0) + (q128, r128), one carry
-        li0 += r128;
-        if (li0 >= Cm1) { li0 -= Cm1; ++i0; }
-        int bl[2], bflg[2], bsti[2], hd[2];
-        T bt[2], bob[2], bcb[2], bcn[2], xl[2];
-        uint64_t blm[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int ii = wi[h];
-          bl[h] = sel(cx.lab, buf)[ii];
-          bflg[h] = sel(cx.flg, buf)[ii];
-          bt[h] = sel(cx.ot, buf)[ii];
-          bob[h] = sel(cx.ob, buf)[ii];
-          bsti[h] = cx.bst[ii];
-          blm[h] = cx.bloom[ii];
-          hd[h] = cx.head[ii];
-          bcb[h] = sel(cx.cb, buf)[ii];
-          bcn[h] = sel(cx.cn, buf)[ii];
-          xl[h] = cx.row[wl[h]];
-        }
-        if (turnw && !(bcast(bt[0], 0) > bottom)) break;   // branch i0's turn: skipped, and all later
-        bool wlive[2];
-        T sw[2], pw[2], batw[2];
-        int slw[2];
-        uint64_t stM[2], wantM[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          wlive[h] = wv[h] && !(bsti[h] & S_DEACT);
-          pw[h] = xl[h] - norm;
-          sw[h] = pw[h] + ((wl[h] == bl[h]) ? bob[h] : bt[h]);
-          slw[h] = lane + 64 * h - wli[h];   // window position where the lane's branch turn starts
-          batw[h] = slw[h] > 0 ? bottom : NI;
-          stM[h] = __ballot(wv[h] && wli[h] == 0 && lane + 64 * h != 0);
-          wantM[h] = __ballot(wlive[h] && ((sw[h] > bottom) | (((blm[h] >> (wl[h] & 63)) & 1ull) != 0)));
-        }
-        if (pc) pc[10] += __builtin_amdgcn_s_memtime() - tc0;
-        if (!(wantM[0] | wantM[1])) {
-          if ((stM[0] & ~__ballot(bt[0] > bottom)) | (stM[1] & ~__ballot(bt[1] > bottom))) break;
-          continue;
-        }
-        int cw[2] = {-1, -1};
-        {
-          int k0 = wlive[0] ? hd[0] : -1, k1 = wlive[1] ? hd[1] : -1;
-          while (__ballot(k0 >= 0 || k1 >= 0)) {
-            int n0 = -1, n1 = -1;
-            if (k0 >= 0) {
-              const int lk = sel(cx.lab, buf)[k0];
-              const int sk = cx.sib[k0];
-              if (lk == wl[0]) cw[0] = k0;
-              else n0 = sk;
-            }
-            if (k1 >= 0) {
-              const int lk = sel(cx.lab, buf)[k1];
-              const int sk = cx.sib[k1];
-              if (lk == wl[1]) cw[1] = k1;
-              else n1 = sk;
-            }
-            k0 = n0;
-            k1 = n1;
+        // the windows run as one loop of their own (each window ends with the
+        // grow's state in registers; the generic chunk path's loop-carried
+        // state stays out of it): from here on the frame's grow is windows only
+        do {
+          // ---- HEAP_SORTED, C <= 64, float: 128-offer windows (two halves of
+          // 64 lanes).  The same offer semantics as the 64-offer chunk below,
+          // with window positions 0..127 in place of lanes: one batch of reads,
+          // one skip test, one child walk and one flush per window, and the
+          // events of the first half, then the second, in one register state.
+          const uint64_t tc0 = pc ? __builtin_amdgcn_s_memtime() : 0;
+          const bool turnw = (li0 == 0);
+          int wi[2], wli[2], wl[2];
+          bool wv[2];
+  #pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int x = li0 + lane + 64 * h;
+            int q = (int)((float)x * rcp);
+            q -= (q * Cm1 > x) ? 1 : 0;
+            q += ((q + 1) * Cm1 <= x) ? 1 : 0;
+            const int iv = i0 + q;
+            wv[h] = iv < nb;
+            wi[h] = wv[h] ? iv : i0;
+            wli[h] = wv[h] ? x - q * Cm1 : 0;
+            wl[h] = wli[h] + (wli[h] >= blank ? 1 : 0);
           }
-        }
-        Best<T> cdw[2];
-        uint64_t NCw[2], LBw[2], RBw[2], donew[2] = {0ull, 0ull};
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const bool isbc = cw[h] >= 0;
-          const int cc = isbc ? cw[h] : wi[h];
-          const bool cev = isbc && (cx.bst[cc] & S_EVICT);
-          const bool recv_fresh = isbc ? (sel(cx.ot, buf)[cc] == NI) : true;
-          const T rs_blank = ((bflg[h] & F_ROOT) && recv_fresh) ? T(0) : NI;
-          cdw[h] = Best<T>{T(0), kBpNone, false};
-          cdw[h].push(((bflg[h] & F_HB) ? bcb[h] : rs_blank) + pw[h],
-                      (bflg[h] & F_HB) ? (((uint32_t)wi[h] << 1) | 0u) : kBpRestart);
-          if (wl[h] != bl[h])
-            cdw[h].push(((bflg[h] & F_HN) ? bcn[h] : NI) + pw[h],
-                        (bflg[h] & F_HN) ? (((uint32_t)wi[h] << 1) | 1u) : kBpRestart);
-          const uint64_t liveM = __ballot(wlive[h]), isbm = __ballot(isbc);
-          NCw[h] = liveM & ~isbm;
-          LBw[h] = liveM & isbm;
-          RBw[h] = LBw[h] & __ballot(cev);
-        }
-        const uint64_t tc1 = pc ? __builtin_amdgcn_s_memtime() : 0;
-        if (pc) { pc[8] += tc1 - tc0; pc[11] += 1; }
-        int mys[2] = {-1, -1};
-        int evr = 0, nv = 0;
-        T fv = front.v;
-        int fs = front.s;
-        int nfree = nextfree;
-        const HeapM geo = heap_m(cx.hdum);
-        const unsigned heb = (unsigned)(uintptr_t)he;
-        const unsigned aj = heb + 8u * (unsigned)(lane + 1), al = heb + 8u * (unsigned)(2 * lane + 2);
-        const unsigned ar = al + 8u, dum = heb + 8u * (unsigned)(cx.hdum + lane);
-        // the events of half H (other half O); rare ones (re-offered branch
-        // children) are decided here, as in the chunk loop below
-#define CTCX_WIN_HALF(H, O)                                                                                       \
-        for (;;) {                                                                                                \
-          int k, cnt = 0;                                                                                         \
-          fv = uni(fv); fs = uni(fs); nfree = uni(nfree); nv = uni(nv);                                           \
-          const uint64_t ta = pc ? __builtin_amdgcn_s_memtime() : 0;                                              \
-          const int est = heap_events2_f32<H == 0>(sw[H], cw[H], slw[H] - 64 * H, cw[O], slw[O] - 64 * H,      \
-                                                   geo.anc, geo.req, aj,                                         \
-                                                   al, ar, dum, mys[H], mys[O], evr, batw[H], batw[O], NCw[H],   \
-                                                   RBw[H], RBw[O], donew[H], LBw[H], LBw[O], fv, fs, nfree, nv,  \
-                                                   uni(nb), 64 * H, k, cnt);                                     \
-          if (pc) { pc[13] += __builtin_amdgcn_s_memtime() - ta; pc[6] += uni(cnt); pc[12] += 1; }             \
-          if (est == 0) break;                                                                                    \
-          k = uni(k);                                                                                             \
-          const uint64_t gtM = __ballot(sw[H] > fv);                                                             \
-          const uint64_t m = ((gtM & NCw[H]) | RBw[H]) & ~donew[H];                                              \
-          if ((__ballot(!(bt[H] > batw[H])) >> k) & 1ull) {                                                      \
-            const int ksl = bcast(slw[H], k);                                                                     \
-            const uint64_t km0 = lowmask(ksl), km1 = ksl > 64 ? lowmask(ksl - 64) : 0ull;                        \
-            NCw[0] &= km0; LBw[0] &= km0; RBw[0] &= km0;                                                          \
-            NCw[1] &= km1; LBw[1] &= km1; RBw[1] &= km1;                                                          \
-            stop = true;                                                                                          \
-            continue;                                                                                             \
-          }                                                                                                       \
-          donew[H] = m ^ (m - 1ull);                                                                              \
-          const int kc = bcast(cw[H], k);                                                                         \
-          if (!((gtM >> k) & 1ull)) {                                                                             \
-            evr = writelane(evr, kc | kDeactRec, nv);                                                             \
-            nv += 1;                                                                                              \
-            const uint64_t dm0 = ~__ballot(wi[0] == kc), dm1 = ~__ballot(wi[1] == kc);                            \
-            NCw[0] &= dm0; LBw[0] &= dm0; RBw[0] &= dm0;                                                          \
-            NCw[1] &= dm1; LBw[1] &= dm1; RBw[1] &= dm1;                                                          \
-            continue;                                                                                             \
-          }                                                                                                       \
-          if (fs < nb) {                                                                                          \
-            evr = writelane(evr, fs, nv);                                                                         \
-            nv += 1;                                                                                              \
-            RBw[0] |= LBw[0] & __ballot(cw[0] == fs);                                                             \
-            RBw[1] |= LBw[1] & __ballot(cw[1] == fs);                                                             \
-          }                                                                                                       \
-          const T k_s = bcast(sw[H], k);                                                                          \
-          mys[0] = (mys[0] == fs) ? -1 : mys[0];                                                                  \
-          mys[1] = (mys[1] == fs) ? -1 : mys[1];                                                                  \
-          mys[H] = __builtin_amdgcn_inverse_ballot_w64(1ull << k) ? kc : mys[H];                                 \
-          HE<T> pL, pR;                                                                                           \
-          pairs_m(he, geo, pL, pR);                                                                               \
-          T c0;                                                                                                   \
-          int s0;                                                                                                 \
-          bool keep;                                                                                              \
-          push_m<T>(he, geo, k_s, kc, pL, pR, c0, s0, keep);                                                      \
-          fv = keep ? k_s : c0;                                                                                   \
-          fs = keep ? kc : s0;                                                                                    \
-          const int kp = k + 64 * H;                                                                              \
-          batw[0] = (slw[0] > kp) ? fv : batw[0];                                                                 \
-          batw[1] = (slw[1] > kp) ? fv : batw[1];                                                                 \
-        }
-        CTCX_WIN_HALF(0, 1)
-        donew[0] = ~0ull;   // the first half's offers are all behind
-        CTCX_WIN_HALF(1, 0)
-#undef CTCX_WIN_HALF
-        front.v = fv;
-        front.s = fs;
-        bottom = fv;
-        nextfree = nfree;
-        // the turn continuing into the next window: skipped -> so is every later one
-        if ((__ballot(wv[1] && !(bt[1] > batw[1])) >> 63) & 1ull) stop = true;
-        const uint64_t q5 = pc ? __builtin_amdgcn_s_memtime() : 0;
-        if (lane < nv) {
-          const int rs = evr & ~kDeactRec;
-          if (evr & kDeactRec) {
-            __hip_atomic_fetch_or(&cx.bst[rs], S_DEACT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          } else {
-            cx.et[rs] = NI; cx.eb[rs] = NI; cx.el[rs] = NI; cx.eflg[rs] = 0;
-            __hip_atomic_fetch_or(&cx.bst[rs], S_EVICT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const int par = sel(cx.par, buf)[rs];
-            if (par >= 0)
-              __hip_atomic_fetch_or(&cx.bloom[par], 1ull << (sel(cx.lab, buf)[rs] & 63), __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_WORKGROUP);
+          i0 += q128;   // 128 offers on: (i0, li0) + (q128, r128), one carry
+          li0 += r128;
+          if (li0 >= Cm1) { li0 -= Cm1; ++i0; }
+          int bl[2], bflg[2], bsti[2], hd[2];
+          T bt[2], bob[2], bcb[2], bcn[2], xl[2];
+          uint64_t blm[2];
+  #pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int ii = wi[h];
+            bl[h] = sel(cx.lab, buf)[ii];
+            bflg[h] = sel(cx.flg, buf)[ii];
+            bt[h] = sel(cx.ot, buf)[ii];
+            bob[h] = sel(cx.ob, buf)[ii];
+            bsti[h] = cx.bst[ii];
+            blm[h] = cx.bloom[ii];
+            hd[h] = cx.head[ii];
+            bcb[h] = sel(cx.cb, buf)[ii];
+            bcn[h] = sel(cx.cn, buf)[ii];
+            xl[h] = cx.row[wl[h]];
           }
-        }
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int ms = mys[h];
-          if (ms >= 0) {
+          if (turnw && !(bcast(bt[0], 0) > bottom)) break;   // branch i0's turn: skipped, and all later
+          bool wlive[2];
+          T sw[2], pw[2], batw[2];
+          int slw[2];
+          uint64_t stM[2], wantM[2];
+  #pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            wlive[h] = wv[h] && !(bsti[h] & S_DEACT);
+            pw[h] = xl[h] - norm;
+            sw[h] = pw[h] + ((wl[h] == bl[h]) ? bob[h] : bt[h]);
+            slw[h] = lane + 64 * h - wli[h];   // window position where the lane's branch turn starts
+            batw[h] = slw[h] > 0 ? bottom : NI;
+            stM[h] = __ballot(wv[h] && wli[h] == 0 && lane + 64 * h != 0);
+            wantM[h] = __ballot(wlive[h] && ((sw[h] > bottom) | (((blm[h] >> (wl[h] & 63)) & 1ull) != 0)));
+          }
+          if (pc) pc[10] += __builtin_amdgcn_s_memtime() - tc0;
+          if (!(wantM[0] | wantM[1])) {
+            if ((stM[0] & ~__ballot(bt[0] > bottom)) | (stM[1] & ~__ballot(bt[1] > bottom))) break;
+            continue;
+          }
+          int cw[2] = {-1, -1};
+          {
+            int k0 = wlive[0] ? hd[0] : -1, k1 = wlive[1] ? hd[1] : -1;
+            while (__ballot(k0 >= 0 || k1 >= 0)) {
+              int n0 = -1, n1 = -1;
+              if (k0 >= 0) {
+                const int lk = sel(cx.lab, buf)[k0];
+                const int sk = cx.sib[k0];
+                if (lk == wl[0]) cw[0] = k0;
+                else n0 = sk;
+              }
+              if (k1 >= 0) {
+                const int lk = sel(cx.lab, buf)[k1];
+                const int sk = cx.sib[k1];
+                if (lk == wl[1]) cw[1] = k1;
+                else n1 = sk;
+              }
+              k0 = n0;
+              k1 = n1;
+            }
+          }
+          Best<T> cdw[2];
+          uint64_t NCw[2], LBw[2], RBw[2], donew[2] = {0ull, 0ull};
+  #pragma unroll
+          for (int h = 0; h < 2; ++h) {
             const bool isbc = cw[h] >= 0;
-            cx.et[ms] = sw[h]; cx.eb[ms] = NI; cx.el[ms] = sw[h];
-            cx.ecn[ms] = cdw[h].p; cx.ebpn[ms] = cdw[h].bp;
-            cx.eflg[ms] = F_HN;
-            cx.ekind[ms] = isbc ? ((uint32_t)cw[h] << 1) : (((uint32_t)wi[h] << 1) | 1u);
-            cx.elab[ms] = wl[h];
-            if (isbc) __hip_atomic_fetch_and(&cx.bst[cw[h]], ~S_EVICT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const int cc = isbc ? cw[h] : wi[h];
+            const bool cev = isbc && (cx.bst[cc] & S_EVICT);
+            const bool recv_fresh = isbc ? (sel(cx.ot, buf)[cc] == NI) : true;
+            const T rs_blank = ((bflg[h] & F_ROOT) && recv_fresh) ? T(0) : NI;
+            cdw[h] = Best<T>{T(0), kBpNone, false};
+            cdw[h].push(((bflg[h] & F_HB) ? bcb[h] : rs_blank) + pw[h],
+                        (bflg[h] & F_HB) ? (((uint32_t)wi[h] << 1) | 0u) : kBpRestart);
+            if (wl[h] != bl[h])
+              cdw[h].push(((bflg[h] & F_HN) ? bcn[h] : NI) + pw[h],
+                          (bflg[h] & F_HN) ? (((uint32_t)wi[h] << 1) | 1u) : kBpRestart);
+            const uint64_t liveM = __ballot(wlive[h]), isbm = __ballot(isbc);
+            NCw[h] = liveM & ~isbm;
+            LBw[h] = liveM & isbm;
+            RBw[h] = LBw[h] & __ballot(cev);
           }
-        }
-        if (pc) pc[15] += __builtin_amdgcn_s_memtime() - q5;
-        if (pc) pc[9] += __builtin_amdgcn_s_memtime() - tc1;
-        continue;
+          const uint64_t tc1 = pc ? __builtin_amdgcn_s_memtime() : 0;
+          if (pc) { pc[8] += tc1 - tc0; pc[11] += 1; }
+          int mys[2] = {-1, -1};
+          int evr = 0, nv = 0;
+          T fv = front.v;
+          int fs = front.s;
+          int nfree = nextfree;
+          const HeapM geo = heap_m(cx.hdum);
+          const unsigned heb = (unsigned)(uintptr_t)he;
+          const unsigned aj = heb + 8u * (unsigned)(lane + 1), al = heb + 8u * (unsigned)(2 * lane + 2);
+          const unsigned ar = al + 8u, dum = heb + 8u * (unsigned)(cx.hdum + lane);
+          // the events of half H (other half O); rare ones (re-offered branch
+          // children) are decided here, as in the chunk loop below
+  #define CTCX_WIN_HALF(H, O)                                                                                       \
+          for (;;) {                                                                                                \
+            int k, cnt = 0;                                                                                         \
+            fv = uni(fv); fs = uni(fs); nfree = uni(nfree); nv = uni(nv);                                           \
+            const uint64_t ta = pc ? __builtin_amdgcn_s_memtime() : 0;                                              \
+            const int est = heap_events2_f32<H == 0>(sw[H], cw[H], slw[H] - 64 * H, cw[O], slw[O] - 64 * H,      \
+                                                     geo.anc, geo.req, aj,                                         \
+                                                     al, ar, dum, mys[H], mys[O], evr, batw[H], batw[O], NCw[H],   \
+                                                     RBw[H], RBw[O], donew[H], LBw[H], LBw[O], fv, fs, nfree, nv,  \
+                                                     uni(nb), 64 * H, k, cnt);                                     \
+            if (pc) { pc[13] += __builtin_amdgcn_s_memtime() - ta; pc[6] += uni(cnt); pc[12] += 1; }             \
+            if (est == 0) break;                                                                                    \
+            k = uni(k);                                                                                             \
+            const uint64_t gtM = __ballot(sw[H] > fv);                                                             \
+            const uint64_t m = ((gtM & NCw[H]) | RBw[H]) & ~donew[H];                                              \
+            if ((__ballot(!(bt[H] > batw[H])) >> k) & 1ull) {                                                      \
+              const int ksl = bcast(slw[H], k);                                                                     \
+              const uint64_t km0 = lowmask(ksl), km1 = ksl > 64 ? lowmask(ksl - 64) : 0ull;                        \
+              NCw[0] &= km0; LBw[0] &= km0; RBw[0] &= km0;                                                          \
+              NCw[1] &= km1; LBw[1] &= km1; RBw[1] &= km1;                                                          \
+              stop = true;                                                                                          \
+              continue;                                                                                             \
+            }                                                                                                       \
+            donew[H] = m ^ (m - 1ull);                                                                              \
+            const int kc = bcast(cw[H], k);                                                                         \
+            if (!((gtM >> k) & 1ull)) {                                                                             \
+              evr = writelane(evr, kc | kDeactRec, nv);                                                             \
+              nv += 1;                                                                                              \
+              const uint64_t dm0 = ~__ballot(wi[0] == kc), dm1 = ~__ballot(wi[1] == kc);                            \
+              NCw[0] &= dm0; LBw[0] &= dm0; RBw[0] &= dm0;                                                          \
+              NCw[1] &= dm1; LBw[1] &= dm1; RBw[1] &= dm1;                                                          \
+              continue;                                                                                             \
+            }                                                                                                       \
+            if (fs < nb) {                                                                                          \
+              evr = writelane(evr, fs, nv);                                                                         \
+              nv += 1;                                                                                              \
+              RBw[0] |= LBw[0] & __ballot(cw[0] == fs);                                                             \
+              RBw[1] |= LBw[1] & __ballot(cw[1] == fs);                                                             \
+            }                                                                                                       \
+            const T k_s = bcast(sw[H], k);                                                                          \
+            mys[0] = (mys[0] == fs) ? -1 : mys[0];                                                                  \
+            mys[1] = (mys[1] == fs) ? -1 : mys[1];                                                                  \
+            mys[H] = __builtin_amdgcn_inverse_ballot_w64(1ull << k) ? kc : mys[H];                                 \
+            HE<T> pL, pR;                                                                                           \
+            pairs_m(he, geo, pL, pR);                                                                               \
+            T c0;                                                                                                   \
+            int s0;                                                                                                 \
+            bool keep;                                                                                              \
+            push_m<T>(he, geo, k_s, kc, pL, pR, c0, s0, keep);                                                      \
+            fv = keep ? k_s : c0;                                                                                   \
+            fs = keep ? kc : s0;                                                                                    \
+            const int kp = k + 64 * H;                                                                              \
+            batw[0] = (slw[0] > kp) ? fv : batw[0];                                                                 \
+            batw[1] = (slw[1] > kp) ? fv : batw[1];                                                                 \
+          }
+          CTCX_WIN_HALF(0, 1)
+          donew[0] = ~0ull;   // the first half's offers are all behind
+          CTCX_WIN_HALF(1, 0)
+  #undef CTCX_WIN_HALF
+          front.v = fv;
+          front.s = fs;
+          bottom = fv;
+          nextfree = nfree;
+          // the turn continuing into the next window: skipped -> so is every later one
+          if ((__ballot(wv[1] && !(bt[1] > batw[1])) >> 63) & 1ull) stop = true;
+          const uint64_t q5 = pc ? __builtin_amdgcn_s_memtime() : 0;
+          if (lane < nv) {
+            const int rs = evr & ~kDeactRec;
+            if (evr & kDeactRec) {
+              __hip_atomic_fetch_or(&cx.bst[rs], S_DEACT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {
+              cx.et[rs] = NI; cx.eb[rs] = NI; cx.el[rs] = NI; cx.eflg[rs] = 0;
+              __hip_atomic_fetch_or(&cx.bst[rs], S_EVICT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              const int par = sel(cx.par, buf)[rs];
+              if (par >= 0)
+                __hip_atomic_fetch_or(&cx.bloom[par], 1ull << (sel(cx.lab, buf)[rs] & 63), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+          }
+  #pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int ms = mys[h];
+            if (ms >= 0) {
+              const bool isbc = cw[h] >= 0;
+              cx.et[ms] = sw[h]; cx.eb[ms] = NI; cx.el[ms] = sw[h];
+              cx.ecn[ms] = cdw[h].p; cx.ebpn[ms] = cdw[h].bp;
+              cx.eflg[ms] = F_HN;
+              cx.ekind[ms] = isbc ? ((uint32_t)cw[h] << 1) : (((uint32_t)wi[h] << 1) | 1u);
+              cx.elab[ms] = wl[h];
+              if (isbc) __hip_atomic_fetch_and(&cx.bst[cw[h]], ~S_EVICT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+          }
+          if (pc) pc[15] += __builtin_amdgcn_s_memtime() - q5;
+          if (pc) pc[9] += __builtin_amdgcn_s_memtime() - tc1;
+        } while (i0 < nb && !stop);
+        break;
       }
     }
     // large C, the beam full: a compacted chunk.  The offers of the span from
