@@ -1265,9 +1265,11 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
       "v_cndmask_b32_e64 v238, v233, v235, s[92:93]\n\t"                                                     \
       "v_bitop3_b32 v239, s92, %[req], %[anc] bitop3:0x28\n\t"   /* (pickR ^ req) & anc */                 \
       "v_cmp_lt_f32_e64 s[96:97], s84, v237\n\t"                                                             \
+      "v_cndmask_b32_e64 v236, %[al], %[ar], s[92:93]\n\t"       /* the min child's address */             \
       "v_readfirstlane_b32 s86, v237\n\t"                                                                    \
       "v_cmp_eq_u32_e64 s[94:95], 0, v239\n\t"                                                               \
       "v_readfirstlane_b32 s87, v238\n\t"                                                                    \
+      "v_cndmask_b32_e64 v236, v236, %[aj], s[96:97]\n\t"        /* v lands here if it is the stop */      \
       "s_and_b32 s98, s92, %[k31]\n\t"                                                                       \
       "s_bitcmp1_b32 s96, 0\n\t"                                                                             \
       "s_cselect_b32 %[fv], s84, s86\n\t"                                                                    \
@@ -1282,16 +1284,14 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
       "s_andn2_b64 s[94:95], s[94:95], s[90:91]\n\t"                                                         \
       "s_andn2_b64 s[90:91], s[94:95], s[96:97]\n\t"                                                         \
       "s_lshl_b64 s[94:95], 1, s86\n\t"                                                                      \
-      "v_cndmask_b32_e32 %[bat], %[bat], v242, vcc\n\t" BAT_OTHER                                           \
-      "v_cndmask_b32_e64 v236, %[al], %[ar], s[92:93]\n\t"                                                   \
       "v_cndmask_b32_e64 v239, %[dum], %[aj], s[90:91]\n\t"                                                  \
-      "v_cndmask_b32_e64 v236, v236, %[aj], s[96:97]\n\t"                                                    \
-      "ds_write2_b32 v239, v237, v238 offset1:1\n\t"                                                         \
       "v_cndmask_b32_e64 v236, %[dum], v236, s[94:95]\n\t"                                                   \
-      "s_and_b64 s[88:89], s[88:89], %[nc]\n\t"                                                              \
-      "s_or_b64 s[88:89], s[88:89], %[rb]\n\t"                                                               \
+      "ds_write2_b32 v239, v237, v238 offset1:1\n\t"                                                         \
       "ds_write2_b32 v236, v240, v241 offset1:1\n\t"                                                         \
       "ds_read_b128 v[232:235], %[al]\n\t"                                                                   \
+      "v_cndmask_b32_e32 %[bat], %[bat], v242, vcc\n\t" BAT_OTHER                                           \
+      "s_and_b64 s[88:89], s[88:89], %[nc]\n\t"                                                              \
+      "s_or_b64 s[88:89], s[88:89], %[rb]\n\t"                                                               \
       "s_and_b64 s[88:89], s[88:89], s[80:81]\n\t"                                                           \
       "s_cbranch_scc0 .Lew_exit_%=\n\t"                                                                      \
       "s_ff1_i32_b64 %[k], s[88:89]\n\t"                                                                     \
@@ -1390,8 +1390,10 @@ __device__ __forceinline__ void extract_f32(unsigned heb, int hi, int lo, int ba
       "v_cndmask_b32_e64 v249, v233, v235, s[92:93]\n\t"   // cs
       "v_bitop3_b32 v251, s92, %[req], %[anc] bitop3:0x28\n\t"
       "v_cmp_lt_f32_e64 s[96:97], v238, v248\n\t"          // gt: min child > v
+      "v_cndmask_b32_e64 v250, %[al], %[ar], s[92:93]\n\t" // the min child's address
       "v_readfirstlane_b32 s86, v249\n\t"                  // s0
       "v_cmp_eq_u32_e64 s[94:95], 0, v251\n\t"             // onp
+      "v_cndmask_b32_e64 v250, v250, %[aj], s[96:97]\n\t"  // v lands here if it is the stop
       "s_and_b32 s98, s92, %[k31]\n\t"
       "s_or_b32 s98, s98, s96\n\t"                         // cnd (low word)
       "s_and_b64 s[88:89], s[94:95], s[98:99]\n\t"         // cm
@@ -1400,14 +1402,12 @@ __device__ __forceinline__ void extract_f32(unsigned heb, int hi, int lo, int ba
       "s_andn2_b64 s[94:95], s[94:95], s[88:89]\n\t"       // live
       "s_andn2_b64 s[88:89], s[94:95], s[96:97]\n\t"       // up
       "s_and_b64 s[80:81], s[94:95], s[98:99]\n\t"         // the stop
-      "v_cndmask_b32_e64 v250, %[al], %[ar], s[92:93]\n\t"
       "v_cndmask_b32_e64 v247, %[dum], %[aj], s[88:89]\n\t"
-      "v_cndmask_b32_e64 v250, v250, %[aj], s[96:97]\n\t"
-      "ds_write2_b32 v247, v248, v249 offset1:1\n\t"
       "v_cndmask_b32_e64 v250, %[dum], v250, s[80:81]\n\t"
+      "ds_write2_b32 v247, v248, v249 offset1:1\n\t"
+      "ds_write2_b32 v250, v238, v239 offset1:1\n\t"
       "s_bitcmp1_b32 s96, 0\n\t"                           // keep: v stays at the root
       "s_cselect_b32 %[fs], s87, s86\n\t"
-      "ds_write2_b32 v250, v238, v239 offset1:1\n\t"
       "s_sub_u32 s84, s84, 1\n\t"
       "s_sub_u32 m0, m0, 1\n\t"
       "s_cmp_gt_i32 s84, %[lo]\n\t"
@@ -1765,8 +1765,10 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
           }
           int cw[2] = {-1, -1};
           {
+            const uint64_t tw0 = pc ? __builtin_amdgcn_s_memtime() : 0;
             int k0 = wlive[0] ? hd[0] : -1, k1 = wlive[1] ? hd[1] : -1;
             while (__ballot(k0 >= 0 || k1 >= 0)) {
+              if (pc) pc[17] += 1;
               int n0 = -1, n1 = -1;
               if (k0 >= 0) {
                 const int lk = sel(cx.lab, buf)[k0];
@@ -1783,6 +1785,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
               k0 = n0;
               k1 = n1;
             }
+            if (pc) pc[18] += __builtin_amdgcn_s_memtime() - tw0;
           }
           Best<T> cdw[2];
           uint64_t NCw[2], LBw[2], RBw[2], donew[2] = {0ull, 0ull};
