@@ -991,71 +991,28 @@ __device__ __forceinline__ int heap_events_f32(float s, int c, int sl, unsigned 
                                                float& bat, uint64_t& NC, uint64_t& RB, uint64_t& done, uint64_t LB,
                                                float& fv, int& fs, int& nfree, int& nv, int nb, int& k, int& cnt) {
   int st;
-  const uint64_t k31 = 0x80000000ull, khi = 0xffffffff00000000ull;
+  const unsigned k31 = 0x80000000u;
   // every scalar operand provably uniform (the asm's "s" constraints)
   NC = uni64(NC); RB = uni64(RB); done = uni64(done); LB = uni64(LB);
   fv = uni(fv); fs = uni(fs); nfree = uni(nfree); nv = uni(nv); nb = uni(nb); cnt = uni(cnt);
   asm volatile(
       "s_mov_b32 %[st], 0\n\t"
+      "s_mov_b32 s99, -1\n\t"                              // cnd's high word: lanes 32..63 always stop
+      "s_not_b64 s[80:81], %[done]\n\t"                    // lanes still to come
       // select the first event
       "v_cmp_lt_f32_e64 s[88:89], %[fv], %[s]\n\t"          // s > front
       "s_and_b64 s[88:89], s[88:89], %[nc]\n\t"
       "s_or_b64 s[88:89], s[88:89], %[rb]\n\t"
-      "s_andn2_b64 s[88:89], s[88:89], %[done]\n\t"        // m (SCC: m != 0)
+      "s_and_b64 s[88:89], s[88:89], s[80:81]\n\t"         // m (SCC: m != 0)
       "s_cbranch_scc0 .Lev_exit_%=\n\t"
       "s_ff1_i32_b64 %[k], s[88:89]\n\t"
       "s_bitcmp1_b64 %[lb], %[k]\n\t"
       "s_cbranch_scc1 .Lev_rare_%=\n\t"
-      "ds_read_b128 v[232:235], %[al]\n\t"                 // its child pairs (L.v, L.s, R.v, R.s)
-      "s_branch .Lev_tail_%=\n"
-      // push of event k (v = s84, slot = s85), then the next selection
-      // interleaved with the push's second half
-      ".Lev_loop_%=:\n\t"
-      CTCX_EVCNT
-      "s_waitcnt lgkmcnt(0)\n\t"
-      "v_cmp_ngt_f32_e64 s[92:93], v234, v232\n\t"         // pickR = !(R > L)
-      "v_mov_b32_e32 v240, s84\n\t"
-      "v_mov_b32_e32 v241, s85\n\t"
-      "v_cndmask_b32_e64 v237, v232, v234, s[92:93]\n\t"   // cv
-      "v_cndmask_b32_e64 v238, v233, v235, s[92:93]\n\t"   // cs
-      "v_bitop3_b32 v239, s92, %[req], %[anc] bitop3:0x28\n\t"
-      "v_cmp_lt_f32_e64 s[96:97], s84, v237\n\t"           // gt: min child > v
-      "v_readfirstlane_b32 s86, v237\n\t"                  // c0: the root's min child
-      "v_cmp_eq_u32_e64 s[94:95], 0, v239\n\t"             // onp: on the root's min-child path
-      "v_readfirstlane_b32 s87, v238\n\t"
-      "s_and_b64 s[98:99], s[92:93], %[k31]\n\t"
-      "s_or_b64 s[98:99], s[98:99], %[khi]\n\t"
-      "s_bitcmp1_b32 s96, 0\n\t"                           // keep: v stays at the root
-      "s_cselect_b32 %[fv], s84, s86\n\t"                  // the new front
-      "s_cselect_b32 %[fs], s85, s87\n\t"
-      "s_or_b64 s[98:99], s[98:99], s[96:97]\n\t"          // cnd: gt, or the min child is a non-lane leaf
-      "v_cmp_lt_i32_e64 vcc, %[k], %[sl]\n\t"              // turns starting after lane k see the new bottom
-      "v_cmp_lt_f32_e64 s[88:89], %[fv], %[s]\n\t"         // next: s > front
-      "s_and_b64 s[90:91], s[94:95], s[98:99]\n\t"         // cm (path nodes meeting the stop condition)
-      "s_ff1_i32_b64 s86, s[90:91]\n\t"                    // the stop: the shallowest of them
-      "v_mov_b32_e32 v242, %[fv]\n\t"
-      "s_lshl_b64 s[90:91], -2, s86\n\t"
-      "s_andn2_b64 s[94:95], s[94:95], s[90:91]\n\t"       // live: path nodes at or above the stop
-      "s_andn2_b64 s[90:91], s[94:95], s[96:97]\n\t"       // up: takes its min child
-      "s_lshl_b64 s[94:95], 1, s86\n\t"                    // the stop
-      "v_cndmask_b32_e32 %[bat], %[bat], v242, vcc\n\t"
-      "v_cndmask_b32_e64 v236, %[al], %[ar], s[92:93]\n\t"
-      "v_cndmask_b32_e64 v239, %[dum], %[aj], s[90:91]\n\t"
-      "v_cndmask_b32_e64 v236, v236, %[aj], s[96:97]\n\t"  // v lands on the stop (gt) or its min child
-      "ds_write2_b32 v239, v237, v238 offset1:1\n\t"
-      "v_cndmask_b32_e64 v236, %[dum], v236, s[94:95]\n\t"
-      "s_and_b64 s[88:89], s[88:89], %[nc]\n\t"
-      "s_or_b64 s[88:89], s[88:89], %[rb]\n\t"
-      "ds_write2_b32 v236, v240, v241 offset1:1\n\t"
-      "ds_read_b128 v[232:235], %[al]\n\t"                 // the next push's child pairs
-      "s_andn2_b64 s[88:89], s[88:89], %[done]\n\t"        // next m
-      "s_cbranch_scc0 .Lev_exit_%=\n\t"
-      "s_ff1_i32_b64 %[k], s[88:89]\n\t"
-      "s_bitcmp1_b64 %[lb], %[k]\n\t"
-      "s_cbranch_scc1 .Lev_rare_%=\n"
+      "ds_read_b128 v[232:235], %[al]\n"                   // its child pairs (L.v, L.s, R.v, R.s)
+      // event k (v = s84, slot = s85): its bookkeeping, then its push, then
+      // the next selection
       ".Lev_tail_%=:\n\t"
-      "s_lshl_b64 s[90:91], -2, %[k]\n\t"
-      "s_not_b64 %[done], s[90:91]\n\t"                    // done = lanes <= k
+      "s_lshl_b64 s[80:81], -2, %[k]\n\t"                  // lanes after k
       "v_readlane_b32 s84, %[s], %[k]\n\t"                 // v = offer k's score
       "s_mov_b32 s85, %[fs]\n\t"                           // slot = the front's
       "s_cmp_lt_i32 %[fs], %[nb]\n\t"
@@ -1065,7 +1022,48 @@ __device__ __forceinline__ int heap_events_f32(float s, int c, int sl, unsigned 
       "s_mov_b32 m0, %[k]\n\t"
       "v_cndmask_b32_e64 %[my], %[my], -1, s[90:91]\n\t"
       "v_writelane_b32 %[my], s85, m0\n\t"                 // lane k: its entry's slot
-      "s_branch .Lev_loop_%=\n"
+      CTCX_EVCNT
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "v_cmp_ngt_f32_e64 s[92:93], v234, v232\n\t"         // pickR = !(R > L)
+      "v_mov_b32_e32 v240, s84\n\t"
+      "v_mov_b32_e32 v241, s85\n\t"
+      "v_cndmask_b32_e64 v237, v232, v234, s[92:93]\n\t"   // cv
+      "v_cndmask_b32_e64 v238, v233, v235, s[92:93]\n\t"   // cs
+      "v_bitop3_b32 v239, s92, %[req], %[anc] bitop3:0x28\n\t"
+      "v_cmp_lt_f32_e64 s[96:97], s84, v237\n\t"           // gt: min child > v
+      "v_cndmask_b32_e64 v236, %[al], %[ar], s[92:93]\n\t" // the min child's address
+      "v_readfirstlane_b32 s86, v237\n\t"                  // c0: the root's min child
+      "v_cmp_eq_u32_e64 s[94:95], 0, v239\n\t"             // onp: on the root's min-child path
+      "v_readfirstlane_b32 s87, v238\n\t"
+      "v_cndmask_b32_e64 v236, v236, %[aj], s[96:97]\n\t"  // v lands on the stop (gt) or its min child
+      "s_and_b32 s98, s92, %[k31]\n\t"
+      "s_bitcmp1_b32 s96, 0\n\t"                           // keep: v stays at the root
+      "s_cselect_b32 %[fv], s84, s86\n\t"                  // the new front
+      "s_cselect_b32 %[fs], s85, s87\n\t"
+      "s_or_b32 s98, s98, s96\n\t"                         // cnd: gt, or the min child is a non-lane leaf
+      "v_cmp_lt_i32_e64 vcc, %[k], %[sl]\n\t"              // turns starting after lane k see the new bottom
+      "v_cmp_lt_f32_e64 s[88:89], %[fv], %[s]\n\t"         // next: s > front
+      "s_and_b64 s[90:91], s[94:95], s[98:99]\n\t"         // cm (path nodes meeting the stop condition)
+      "s_ff1_i32_b64 s86, s[90:91]\n\t"                    // the stop: the shallowest of them
+      "v_mov_b32_e32 v242, %[fv]\n\t"
+      "s_lshl_b64 s[90:91], -2, s86\n\t"
+      "s_andn2_b64 s[94:95], s[94:95], s[90:91]\n\t"       // live: path nodes at or above the stop
+      "s_andn2_b64 s[90:91], s[94:95], s[96:97]\n\t"       // up: takes its min child
+      "s_lshl_b64 s[94:95], 1, s86\n\t"                    // the stop
+      "v_cndmask_b32_e64 v239, %[dum], %[aj], s[90:91]\n\t"
+      "v_cndmask_b32_e64 v236, %[dum], v236, s[94:95]\n\t"
+      "ds_write2_b32 v239, v237, v238 offset1:1\n\t"
+      "ds_write2_b32 v236, v240, v241 offset1:1\n\t"
+      "ds_read_b128 v[232:235], %[al]\n\t"                 // the next push's child pairs
+      "v_cndmask_b32_e32 %[bat], %[bat], v242, vcc\n\t"
+      "s_and_b64 s[88:89], s[88:89], %[nc]\n\t"
+      "s_or_b64 s[88:89], s[88:89], %[rb]\n\t"
+      "s_and_b64 s[88:89], s[88:89], s[80:81]\n\t"         // next m
+      "s_cbranch_scc0 .Lev_exit_%=\n\t"
+      "s_ff1_i32_b64 %[k], s[88:89]\n\t"
+      "s_bitcmp1_b64 %[lb], %[k]\n\t"
+      "s_cbranch_scc0 .Lev_tail_%=\n\t"                    // the next push, unless k is rare
+      "s_branch .Lev_rare_%=\n"
       // the evicted front is a branch's entry: a fresh slot; record the
       // eviction; a live re-offer of that branch is now wanted
       ".Lev_evb_%=:\n\t"
@@ -1081,14 +1079,15 @@ __device__ __forceinline__ int heap_events_f32(float s, int c, int sl, unsigned 
       ".Lev_rare_%=:\n\t"
       "s_mov_b32 %[st], 1\n"
       ".Lev_exit_%=:\n\t"
+      "s_not_b64 %[done], s[80:81]\n\t"
       "s_waitcnt lgkmcnt(0)"
       : [my] "+v"(myslot), [evr] "+v"(evr), [bat] "+v"(bat), [nc] "+s"(NC), [rb] "+s"(RB), [done] "+s"(done),
         [fv] "+s"(fv), [fs] "+s"(fs), [nfree] "+s"(nfree), [nv] "+s"(nv), [k] "=&s"(k), [st] "=&s"(st), [cnt] "+s"(cnt)
       : [s] "v"(s), [c] "v"(c), [sl] "v"(sl), [anc] "v"(anc), [req] "v"(req), [aj] "v"(aj), [al] "v"(al),
-        [ar] "v"(ar), [dum] "v"(dum), [lb] "s"(LB), [nb] "s"(nb), [k31] "s"(k31), [khi] "s"(khi)
-      : "memory", "vcc", "m0", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96",
-        "s97", "s98", "s99", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239", "v240", "v241",
-        "v242", "v243");
+        [ar] "v"(ar), [dum] "v"(dum), [lb] "s"(LB), [nb] "s"(nb), [k31] "s"(k31)
+      : "memory", "vcc", "m0", "s80", "s81", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93",
+        "s94", "s95", "s96", "s97", "s98", "s99", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239",
+        "v240", "v241", "v242", "v243");
   return st;
 }
 
@@ -1115,18 +1114,28 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
   fv = uni(fv); fs = uni(fs); nfree = uni(nfree); nv = uni(nv); nb = uni(nb); cnt = uni(cnt);
   asm volatile(
       "s_mov_b32 %[st], 0\n\t"
+      "s_not_b64 s[80:81], %[done]\n\t"                    // lanes still to come
       "v_cmp_lt_f32_e64 s[88:89], %[fv], %[s]\n\t"          // s > front
       "s_and_b64 s[88:89], s[88:89], %[nc]\n\t"
       "s_or_b64 s[88:89], s[88:89], %[rb]\n\t"
-      "s_andn2_b64 s[88:89], s[88:89], %[done]\n\t"        // m (SCC: m != 0)
+      "s_and_b64 s[88:89], s[88:89], s[80:81]\n\t"         // m (SCC: m != 0)
       "s_cbranch_scc0 .Lem_exit_%=\n\t"
       "s_ff1_i32_b64 %[k], s[88:89]\n\t"
       "s_bitcmp1_b64 %[lb], %[k]\n\t"
       "s_cbranch_scc1 .Lem_rare_%=\n\t"
       "ds_read_b128 v[232:235], %[al]\n\t"                 // group 0 child pairs
-      "ds_read_b128 v[244:247], %[al] offset:1024\n\t"     // group 1 child pairs
-      "s_branch .Lem_tail_%=\n"
-      ".Lem_loop_%=:\n\t"
+      "ds_read_b128 v[244:247], %[al] offset:1024\n"       // group 1 child pairs
+      ".Lem_tail_%=:\n\t"
+      "s_lshl_b64 s[80:81], -2, %[k]\n\t"                  // lanes after k
+      "v_readlane_b32 s84, %[s], %[k]\n\t"                 // v = offer k's score
+      "s_mov_b32 s85, %[fs]\n\t"                           // slot = the front's
+      "s_cmp_lt_i32 %[fs], %[nb]\n\t"
+      "s_cbranch_scc1 .Lem_evb_%=\n"
+      ".Lem_slot_%=:\n\t"
+      "v_cmp_eq_u32_e64 s[90:91], %[fs], %[my]\n\t"        // an entry accepted in this chunk is the evicted front
+      "s_mov_b32 m0, %[k]\n\t"
+      "v_cndmask_b32_e64 %[my], %[my], -1, s[90:91]\n\t"
+      "v_writelane_b32 %[my], s85, m0\n\t"                 // lane k: its entry's slot
       CTCX_EVCNT
       "s_waitcnt lgkmcnt(0)\n\t"
       "v_cmp_ngt_f32_e64 s[92:93], v234, v232\n\t"         // pR0 = !(R > L)
@@ -1145,8 +1154,11 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
       "v_or_b32_e32 v248, v248, v249\n\t"
       "v_cndmask_b32_e64 v250, v244, v246, %[p1]\n\t"      // cv1
       "v_cndmask_b32_e64 v251, v245, v247, %[p1]\n\t"      // cs1
+      "v_cndmask_b32_e64 v236, %[al], %[ar], s[92:93]\n\t" // group 0's min-child address
       "v_cmp_eq_u32_e64 %[o1], 0, v248\n\t"                // onp1
       "v_cmp_lt_f32_e64 %[g1], s84, v250\n\t"              // gt1
+      "v_cndmask_b32_e64 v236, v236, %[aj], s[96:97]\n\t"  // v lands on the stop (gt) or its min child
+      "v_cndmask_b32_e64 v253, %[al1], %[ar1], %[p1]\n\t"
       "s_and_b64 s[98:99], s[92:93], %[k63]\n\t"
       "s_or_b64 s[98:99], s[98:99], s[96:97]\n\t"          // cnd0
       "s_bitcmp1_b32 s96, 0\n\t"                           // keep: v stays at the root
@@ -1154,6 +1166,7 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
       "s_cselect_b32 %[fs], s85, s87\n\t"
       "v_cmp_lt_i32_e64 vcc, %[k], %[sl]\n\t"              // turns starting after lane k see the new bottom
       "v_cmp_lt_f32_e64 s[88:89], %[fv], %[s]\n\t"         // next: s > front
+      "v_cndmask_b32_e64 v253, v253, %[aj1], %[g1]\n\t"
       "s_and_b64 s[90:91], s[94:95], s[98:99]\n\t"         // cm0
       "s_cmp_eq_u64 s[90:91], 0\n\t"
       "s_cselect_b64 %[o1], %[o1], 0\n\t"                  // live1: the path's group-1 node, when group 0 has no stop
@@ -1163,42 +1176,26 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
       "s_andn2_b64 s[94:95], s[94:95], s[90:91]\n\t"       // live0
       "s_andn2_b64 s[90:91], s[94:95], s[96:97]\n\t"       // up0
       "s_and_b64 s[94:95], s[94:95], s[98:99]\n\t"         // stop0 = live0 & cnd0
-      "v_cndmask_b32_e32 %[bat], %[bat], v242, vcc\n\t"
-      "v_cndmask_b32_e64 v236, %[al], %[ar], s[92:93]\n\t"
       "v_cndmask_b32_e64 v239, %[dum], %[aj], s[90:91]\n\t"
-      "v_cndmask_b32_e64 v236, v236, %[aj], s[96:97]\n\t"  // v lands on the stop (gt) or its min child
-      "ds_write2_b32 v239, v237, v238 offset1:1\n\t"
-      "v_cndmask_b32_e64 v236, %[dum], v236, s[94:95]\n\t"
       "s_andn2_b64 s[90:91], %[o1], %[g1]\n\t"             // up1
-      "v_cndmask_b32_e64 v253, %[al1], %[ar1], %[p1]\n\t"
-      "ds_write2_b32 v236, v240, v241 offset1:1\n\t"
-      "v_cndmask_b32_e64 v253, v253, %[aj1], %[g1]\n\t"
-      "v_cndmask_b32_e64 v252, %[dum], %[aj1], s[90:91]\n\t"
+      "v_cndmask_b32_e64 v236, %[dum], v236, s[94:95]\n\t"
       "v_cndmask_b32_e64 v253, %[dum], v253, %[o1]\n\t"    // group 1's stop is its live node
+      "v_cndmask_b32_e64 v252, %[dum], %[aj1], s[90:91]\n\t"
+      "ds_write2_b32 v239, v237, v238 offset1:1\n\t"
+      "ds_write2_b32 v236, v240, v241 offset1:1\n\t"
       "ds_write2_b32 v252, v250, v251 offset1:1\n\t"
-      "s_and_b64 s[88:89], s[88:89], %[nc]\n\t"
-      "s_or_b64 s[88:89], s[88:89], %[rb]\n\t"
       "ds_write2_b32 v253, v240, v241 offset1:1\n\t"
       "ds_read_b128 v[232:235], %[al]\n\t"                 // the next push's child pairs
       "ds_read_b128 v[244:247], %[al] offset:1024\n\t"
-      "s_andn2_b64 s[88:89], s[88:89], %[done]\n\t"        // next m
+      "v_cndmask_b32_e32 %[bat], %[bat], v242, vcc\n\t"
+      "s_and_b64 s[88:89], s[88:89], %[nc]\n\t"
+      "s_or_b64 s[88:89], s[88:89], %[rb]\n\t"
+      "s_and_b64 s[88:89], s[88:89], s[80:81]\n\t"         // next m
       "s_cbranch_scc0 .Lem_exit_%=\n\t"
       "s_ff1_i32_b64 %[k], s[88:89]\n\t"
       "s_bitcmp1_b64 %[lb], %[k]\n\t"
-      "s_cbranch_scc1 .Lem_rare_%=\n"
-      ".Lem_tail_%=:\n\t"
-      "s_lshl_b64 s[90:91], -2, %[k]\n\t"
-      "s_not_b64 %[done], s[90:91]\n\t"                    // done = lanes <= k
-      "v_readlane_b32 s84, %[s], %[k]\n\t"                 // v = offer k's score
-      "s_mov_b32 s85, %[fs]\n\t"                           // slot = the front's
-      "s_cmp_lt_i32 %[fs], %[nb]\n\t"
-      "s_cbranch_scc1 .Lem_evb_%=\n"
-      ".Lem_slot_%=:\n\t"
-      "v_cmp_eq_u32_e64 s[90:91], %[fs], %[my]\n\t"        // an entry accepted in this chunk is the evicted front
-      "s_mov_b32 m0, %[k]\n\t"
-      "v_cndmask_b32_e64 %[my], %[my], -1, s[90:91]\n\t"
-      "v_writelane_b32 %[my], s85, m0\n\t"                 // lane k: its entry's slot
-      "s_branch .Lem_loop_%=\n"
+      "s_cbranch_scc0 .Lem_tail_%=\n\t"                    // the next push, unless k is rare
+      "s_branch .Lem_rare_%=\n"
       ".Lem_evb_%=:\n\t"
       "s_mov_b32 s85, %[nfree]\n\t"
       "s_add_u32 %[nfree], %[nfree], 1\n\t"
@@ -1212,6 +1209,7 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
       ".Lem_rare_%=:\n\t"
       "s_mov_b32 %[st], 1\n"
       ".Lem_exit_%=:\n\t"
+      "s_not_b64 %[done], s[80:81]\n\t"
       "s_waitcnt lgkmcnt(0)"
       : [my] "+v"(myslot), [evr] "+v"(evr), [bat] "+v"(bat), [nc] "+s"(NC), [rb] "+s"(RB), [done] "+s"(done),
         [fv] "+s"(fv), [fs] "+s"(fs), [nfree] "+s"(nfree), [nv] "+s"(nv), [k] "=&s"(k), [st] "=&s"(st),
@@ -1219,9 +1217,9 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
       : [s] "v"(s), [c] "v"(c), [sl] "v"(sl), [anc] "v"(anc), [req] "v"(req), [an1l] "v"(an1l), [an1h] "v"(an1h),
         [rq1l] "v"(rq1l), [rq1h] "v"(rq1h), [aj] "v"(aj), [al] "v"(al), [ar] "v"(ar), [aj1] "v"(aj1),
         [al1] "v"(al1), [ar1] "v"(ar1), [dum] "v"(dum), [lb] "s"(LB), [nb] "s"(nb), [k63] "s"(k63)
-      : "memory", "vcc", "m0", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95", "s96",
-        "s97", "s98", "s99", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239", "v240", "v241",
-        "v242", "v243", "v244", "v245", "v246", "v247", "v248", "v249", "v250", "v251", "v252", "v253");
+      : "memory", "vcc", "m0", "s80", "s81", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93",
+        "s94", "s95", "s96", "s97", "s98", "s99", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239",
+        "v240", "v241", "v242", "v243", "v244", "v245", "v246", "v247", "v248", "v249", "v250", "v251", "v252", "v253");
   return st;
 }
 
@@ -1440,17 +1438,17 @@ __device__ __forceinline__ void extract_m2_f32(unsigned heb, int hi, int lo, int
   heb = (unsigned)uni((int)heb); hi = uni(hi); lo = uni(lo); base = uni(base); fs = uni(fs);
   asm volatile(
       "s_mov_b32 s84, %[hi]\n\t"
-      "s_mov_b64 s[90:91], 1\n\t"                          // lane 0
-      "v_mov_b32_e32 v242, 0x7f800000\n\t"                 // the sentinel (+inf, -1)
-      "v_mov_b32_e32 v243, -1\n"
-      "s_lshl_b32 s85, s84, 3\n\t"
-      "s_add_u32 s85, s85, %[heb]\n\t"
-      "v_mov_b32_e32 v236, s85\n\t"                      // he[len]: position len - 1 (-8 B per pop)
-      "s_sub_u32 s86, s84, 1\n\t"
-      "s_sub_u32 m0, s86, %[base]\n\t"                    // its lane in srt (-1 per pop)
-      ".Ly_top_%=:\n\t"
       "s_cmp_le_i32 s84, %[lo]\n\t"
       "s_cbranch_scc1 .Ly_end_%=\n\t"
+      "s_mov_b64 s[90:91], 1\n\t"                          // lane 0
+      "v_mov_b32_e32 v242, 0x7f800000\n\t"                 // the sentinel (+inf, -1)
+      "v_mov_b32_e32 v243, -1\n\t"
+      "s_lshl_b32 s85, s84, 3\n\t"
+      "s_add_u32 s85, s85, %[heb]\n\t"
+      "v_mov_b32_e32 v236, s85\n\t"                        // he[len]: position len - 1 (-8 B per pop)
+      "s_sub_u32 s86, s84, 1\n\t"
+      "s_sub_u32 m0, s86, %[base]\n"                       // its lane in srt (-1 per pop)
+      ".Ly_top_%=:\n\t"
       "ds_read_b64 v[238:239], v236\n\t"                   // e[len - 1] (every lane: broadcast)
       "v_cndmask_b32_e64 v241, %[dum], v236, s[90:91]\n\t"
       "v_writelane_b32 %[srt], %[fs], m0\n\t"              // the front: position len - 1
@@ -1460,20 +1458,22 @@ __device__ __forceinline__ void extract_m2_f32(unsigned heb, int hi, int lo, int
       "s_waitcnt lgkmcnt(0)\n\t"
       "v_cmp_ngt_f32_e64 s[92:93], v234, v232\n\t"         // pR0
       "v_cmp_ngt_f32_e64 %[p1], v254, v252\n\t"            // pR1
-      "v_mov_b32_e32 v244, v238\n\t"
-      "v_mov_b32_e32 v245, v239\n\t"
+      "v_readfirstlane_b32 s87, v239\n\t"                  // v's slot
+      "v_subrev_u32_e32 v236, 8, v236\n\t"
       "v_cndmask_b32_e64 v248, v232, v234, s[92:93]\n\t"   // cv0
       "v_cndmask_b32_e64 v249, v233, v235, s[92:93]\n\t"   // cs0
       "v_bitop3_b32 v251, s92, %[req], %[anc] bitop3:0x28\n\t"
       "v_cmp_lt_f32_e64 s[96:97], v238, v248\n\t"          // gt0: min child > v
-      "v_readfirstlane_b32 s87, v239\n\t"                  // v's slot
+      "v_cndmask_b32_e64 v250, %[al], %[ar], s[92:93]\n\t" // group 0's min-child address
       "v_cmp_eq_u32_e64 s[94:95], 0, v251\n\t"             // onp0
       "v_readfirstlane_b32 s86, v249\n\t"                  // s0
       "v_bitop3_b32 %[t0], s92, %[rq1l], %[an1l] bitop3:0x28\n\t"
       "v_bitop3_b32 %[t1], s93, %[rq1h], %[an1h] bitop3:0x28\n\t"
+      "v_cndmask_b32_e64 v250, v250, %[aj], s[96:97]\n\t"
       "v_or_b32_e32 %[t0], %[t0], %[t1]\n\t"
       "v_cndmask_b32_e64 %[c1v], v252, v254, %[p1]\n\t"    // cv1
       "v_cndmask_b32_e64 %[c1s], v253, v255, %[p1]\n\t"    // cs1
+      "v_cndmask_b32_e64 %[a1], %[al1], %[ar1], %[p1]\n\t"
       "v_cmp_eq_u32_e64 %[o1], 0, %[t0]\n\t"               // onp1
       "v_cmp_lt_f32_e64 %[g1], v238, %[c1v]\n\t"           // gt1
       "s_and_b64 s[98:99], s[92:93], %[k63]\n\t"
@@ -1482,29 +1482,26 @@ __device__ __forceinline__ void extract_m2_f32(unsigned heb, int hi, int lo, int
       "s_cmp_eq_u64 s[88:89], 0\n\t"
       "s_cselect_b64 %[o1], %[o1], 0\n\t"                  // live1
       "s_ff1_i32_b64 s88, s[88:89]\n\t"                    // the stop (-1: in group 1)
+      "v_cndmask_b32_e64 %[a1], %[a1], %[aj1], %[g1]\n\t"
       "s_lshl_b64 s[88:89], -2, s88\n\t"
       "s_andn2_b64 s[94:95], s[94:95], s[88:89]\n\t"       // live0
       "s_andn2_b64 s[88:89], s[94:95], s[96:97]\n\t"       // up0
       "s_and_b64 s[98:99], s[94:95], s[98:99]\n\t"         // stop0 = live0 & cnd0
-      "v_cndmask_b32_e64 v250, %[al], %[ar], s[92:93]\n\t"
       "v_cndmask_b32_e64 v247, %[dum], %[aj], s[88:89]\n\t"
-      "v_cndmask_b32_e64 v250, v250, %[aj], s[96:97]\n\t"
-      "ds_write2_b32 v247, v248, v249 offset1:1\n\t"
-      "v_cndmask_b32_e64 v250, %[dum], v250, s[98:99]\n\t"
       "s_andn2_b64 s[88:89], %[o1], %[g1]\n\t"             // up1
-      "v_cndmask_b32_e64 %[a1], %[al1], %[ar1], %[p1]\n\t"
-      "ds_write2_b32 v250, v244, v245 offset1:1\n\t"
-      "v_cndmask_b32_e64 %[a1], %[a1], %[aj1], %[g1]\n\t"
-      "v_cndmask_b32_e64 %[u1], %[dum], %[aj1], s[88:89]\n\t"
+      "v_cndmask_b32_e64 v250, %[dum], v250, s[98:99]\n\t"
       "v_cndmask_b32_e64 %[a1], %[dum], %[a1], %[o1]\n\t"  // group 1's stop is its live node
+      "v_cndmask_b32_e64 %[u1], %[dum], %[aj1], s[88:89]\n\t"
+      "ds_write2_b32 v247, v248, v249 offset1:1\n\t"
+      "ds_write2_b32 v250, v238, v239 offset1:1\n\t"
       "ds_write2_b32 %[u1], %[c1v], %[c1s] offset1:1\n\t"
-      "ds_write2_b32 %[a1], v244, v245 offset1:1\n\t"
+      "ds_write2_b32 %[a1], v238, v239 offset1:1\n\t"
       "s_bitcmp1_b32 s96, 0\n\t"                           // keep: v stays at the root
       "s_cselect_b32 %[fs], s87, s86\n\t"
       "s_sub_u32 s84, s84, 1\n\t"
       "s_sub_u32 m0, m0, 1\n\t"
-      "v_subrev_u32_e32 v236, 8, v236\n\t"
-      "s_branch .Ly_top_%=\n"
+      "s_cmp_gt_i32 s84, %[lo]\n\t"
+      "s_cbranch_scc1 .Ly_top_%=\n"
       ".Ly_end_%=:\n\t"
       "s_waitcnt lgkmcnt(0)"
       : [srt] "+v"(srt), [fs] "+s"(fs), [p1] "=&s"(p1), [g1] "=&s"(g1), [o1] "=&s"(o1), [t0] "=&v"(t0),
