@@ -1789,9 +1789,11 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
   #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const bool isbc = cw[h] >= 0;
-            const int cc = isbc ? cw[h] : wi[h];
-            const bool cev = isbc && (cx.bst[cc] & S_EVICT);
-            const bool recv_fresh = isbc ? (sel(cx.ot, buf)[cc] == NI) : true;
+            bool cev = false, recv_fresh = true;
+            if (isbc) {   // the offer's child is a branch (few lanes, most windows none): its state
+              cev = (cx.bst[cw[h]] & S_EVICT) != 0;
+              recv_fresh = sel(cx.ot, buf)[cw[h]] == NI;
+            }
             const T rs_blank = ((bflg[h] & F_ROOT) && recv_fresh) ? T(0) : NI;
             cdw[h] = Best<T>{T(0), kBpNone, false};
             cdw[h].push(((bflg[h] & F_HB) ? bcb[h] : rs_blank) + pw[h],
