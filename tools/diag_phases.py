@@ -23,7 +23,8 @@ m = buf.astype(np.float64).mean(0)
 fr = m[7]
 names = ["rowload", "recursion", "grow", "extract", "commit", "literal", "heap events", "frames",
          "scoring", "eventloop", "score:pre-skip", "chunks", "asm calls", "asm loop", "makeheap", "flush",
-         "gather (C>64)", "gather: window steps", "gather: windows", "gather: top set",
+         "gather (C>64)", "gather: window steps | C<=64: child-walk steps", "gather: windows | C<=64: child walk",
+         "gather: top set",
          "gather: branch select", "gather: branches", "gather: S branches", "gather: select+S test+S hot"]
 CYC = {0, 1, 2, 3, 4, 5, 8, 9, 10, 13, 14, 15, 16, 18, 19, 20, 23}
 print("B=%d T=%d W=%d P=%d C=%d decode_ms=%.1f" % (B, T, W, P, C, d.last_stats["decode_kernel_ms"]))
