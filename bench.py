@@ -224,6 +224,8 @@ def main():
     ap.add_argument("--no-host-io", action="store_true", help="skip the host-I/O (PCIe-inclusive) extra")
     ap.add_argument("--seq-len", type=int, default=0, help="diagnostics: override T (not a bench line)")
     ap.add_argument("--batch-per-gpu", type=int, default=0, help="diagnostics: override B per GPU (not a bench line)")
+    ap.add_argument("--scorer", choices=["base", "bigram"], default="base",
+                    help="diagnostics: the bigram beam scorer with a random <= 0 table (not a bench line)")
     ap.add_argument("--record-ring", action="store_true",
                     help="diagnostics: the LDS record ring (only reachable beam records written to HBM)")
     ap.add_argument("--no-strong", action="store_true",
@@ -267,13 +269,17 @@ def main():
 
     flags = _lib.CTCEXT_FLAG_PROFILE | (_lib.CTCEXT_FLAG_RECORD_RING if args.record_ring else 0)
     dec = ctcext_amd.get_decoder(local)
+    skw = {}
+    if args.scorer == "bigram":   # ctc_beam_scorer.h's hook with a bigram table of log-probabilities
+        g = torch.Generator(device=dev).manual_seed(7)
+        skw["scorer_table"] = -torch.rand((C + 1, C), generator=g, device=dev, dtype=torch.float32) * 2.0
 
     def step(outputs="host"):
         # 8(d): device-resident logits in, SparseTensor components on the host
         # out (world > 1: device outputs, gathered over RCCL to rank 0)
         out = ctcext_amd.ctc_ext_beam_search_decoder(x, sl, W, P, merge_repeated=merge,
                                                      blank_index=blank, blank_label=-1, flags=flags,
-                                                     outputs=outputs if world == 1 else "device")
+                                                     outputs=outputs if world == 1 else "device", **skw)
         if world > 1 and not args.no_gather:
             got = gather_to_root(out, rank * B, P)
             if got is not None:   # rank 0: the whole batch's components to the host
@@ -321,9 +327,9 @@ def main():
             traffic_src = "stale: %s is of build %s, this is %s" % (os.path.relpath(pmc, ROOT),
                                                                    pj.get("lib_sha16"), lib_hash())
     metric = "decoded frames/sec at B=256, T=1500, C=29, beam_width=128; 1/2/4/8 GPUs"   # BASELINE.json
-    if args.config != "cfg3" or args.seq_len or args.batch_per_gpu:   # diagnostics lines name their own workload
-        metric = "decoded frames/sec at B=%d, T=%d, C=%d, beam_width=%d (%s, not the BASELINE metric)" % (
-            B * world, T, C, W, args.config)
+    if args.config != "cfg3" or args.seq_len or args.batch_per_gpu or args.scorer != "base":   # diagnostics
+        metric = "decoded frames/sec at B=%d, T=%d, C=%d, beam_width=%d (%s%s, not the BASELINE metric)" % (
+            B * world, T, C, W, args.config, ", bigram scorer" if args.scorer != "base" else "")
     res = {
         "metric": metric,
         "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
