@@ -1249,7 +1249,17 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
       "v_readlane_b32 s84, %[s], %[k]\n\t"                                                                   \
       "s_mov_b32 s85, %[fs]\n\t"                                                                             \
       "s_cmp_lt_i32 %[fs], %[nb]\n\t"                                                                        \
-      "s_cbranch_scc1 .Lew_evb_%=\n"                                                                         \
+      "s_cbranch_scc0 .Lew_slot_%=\n\t"                    /* the front is a new child's entry */         \
+      /* the evicted front is a branch's entry: a fresh slot, the eviction */                                 \
+      /* recorded, a live re-offer of that branch now wanted */                                                \
+      "s_mov_b32 s85, %[nfree]\n\t"                                                                          \
+      "s_add_u32 %[nfree], %[nfree], 1\n\t"                                                                  \
+      "s_mov_b32 m0, %[nv]\n\t"                                                                              \
+      "s_add_u32 %[nv], %[nv], 1\n\t"                                                                        \
+      "v_writelane_b32 %[evr], %[fs], m0\n\t"                                                                \
+      "v_cmp_eq_u32_e64 s[90:91], %[fs], %[c]\n\t"                                                           \
+      "s_and_b64 s[90:91], s[90:91], %[lb]\n\t"                                                              \
+      "s_or_b64 %[rb], %[rb], s[90:91]\n\t" EVB_OTHER                                                        \
       ".Lew_slot_%=:\n\t"                                                                                    \
       "v_cmp_eq_u32_e64 s[90:91], %[fs], %[my]\n\t" MYO_CMP                                                  \
       "s_mov_b32 m0, %[k]\n\t"                                                                               \
@@ -1295,17 +1305,6 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
       "s_ff1_i32_b64 %[k], s[88:89]\n\t"                                                                     \
       "s_bitcmp1_b64 %[lb], %[k]\n\t"                                                                        \
       "s_cbranch_scc0 .Lew_tail_%=\n\t"                     /* the next push, unless k is rare */            \
-      "s_branch .Lew_rare_%=\n"                                                                              \
-      ".Lew_evb_%=:\n\t"                                                                                     \
-      "s_mov_b32 s85, %[nfree]\n\t"                                                                          \
-      "s_add_u32 %[nfree], %[nfree], 1\n\t"                                                                  \
-      "s_mov_b32 m0, %[nv]\n\t"                                                                              \
-      "s_add_u32 %[nv], %[nv], 1\n\t"                                                                        \
-      "v_writelane_b32 %[evr], %[fs], m0\n\t"                                                                \
-      "v_cmp_eq_u32_e64 s[90:91], %[fs], %[c]\n\t"                                                           \
-      "s_and_b64 s[90:91], s[90:91], %[lb]\n\t"                                                              \
-      "s_or_b64 %[rb], %[rb], s[90:91]\n\t" EVB_OTHER                                                        \
-      "s_branch .Lew_slot_%=\n"                                                                              \
       ".Lew_rare_%=:\n\t"                                                                                    \
       "s_mov_b32 %[st], 1\n"                                                                                 \
       ".Lew_exit_%=:\n\t"                                                                                    \
