@@ -1025,8 +1025,7 @@ __device__ __forceinline__ int heap_events_f32(float s, int c, int sl, unsigned 
       CTCX_EVCNT
       "s_waitcnt lgkmcnt(0)\n\t"
       "v_cmp_ngt_f32_e64 s[92:93], v234, v232\n\t"         // pickR = !(R > L)
-      "v_mov_b32_e32 v240, s84\n\t"
-      "v_mov_b32_e32 v241, s85\n\t"
+      "v_mov_b64_e32 v[240:241], s[84:85]\n\t"
       "v_cndmask_b32_e64 v237, v232, v234, s[92:93]\n\t"   // cv
       "v_cndmask_b32_e64 v238, v233, v235, s[92:93]\n\t"   // cs
       "v_bitop3_b32 v239, s92, %[req], %[anc] bitop3:0x28\n\t"
@@ -1140,8 +1139,7 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
       "s_waitcnt lgkmcnt(0)\n\t"
       "v_cmp_ngt_f32_e64 s[92:93], v234, v232\n\t"         // pR0 = !(R > L)
       "v_cmp_ngt_f32_e64 %[p1], v246, v244\n\t"            // pR1
-      "v_mov_b32_e32 v240, s84\n\t"
-      "v_mov_b32_e32 v241, s85\n\t"
+      "v_mov_b64_e32 v[240:241], s[84:85]\n\t"
       "v_cndmask_b32_e64 v237, v232, v234, s[92:93]\n\t"   // cv0
       "v_cndmask_b32_e64 v238, v233, v235, s[92:93]\n\t"   // cs0
       "v_bitop3_b32 v239, s92, %[req], %[anc] bitop3:0x28\n\t"
@@ -1267,8 +1265,7 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
       "v_writelane_b32 %[my], s85, m0\n\t" CTCX_EVCNT                                                        \
       "s_waitcnt lgkmcnt(0)\n\t"                                                                             \
       "v_cmp_ngt_f32_e64 s[92:93], v234, v232\n\t"                                                           \
-      "v_mov_b32_e32 v240, s84\n\t"                                                                          \
-      "v_mov_b32_e32 v241, s85\n\t"                                                                          \
+      "v_mov_b64_e32 v[240:241], s[84:85]\n\t"                                                                          \
       "v_cndmask_b32_e64 v237, v232, v234, s[92:93]\n\t"                                                     \
       "v_cndmask_b32_e64 v238, v233, v235, s[92:93]\n\t"                                                     \
       "v_bitop3_b32 v239, s92, %[req], %[anc] bitop3:0x28\n\t"   /* (pickR ^ req) & anc */                 \
