@@ -138,7 +138,7 @@ def cpu_baseline(cfg, n_workers, t_cap):
                                       "same container type, cfg3-shape item"}}
 
 
-def strong_scaling(args, cfg, world, rank, dev, dec, gather_to_root):
+def strong_scaling(args, cfg, world, rank, dev, dec, gather_to_root, x):
     """The metric's literal case, a FIXED global batch (BASELINE.json: B=256 on
     1/2/4/8 GPUs; kernels.cc:68-90 loops over it on one core).
     N>1: measured -- the global batch (seed 20251015) is split into contiguous
@@ -152,8 +152,18 @@ def strong_scaling(args, cfg, world, rank, dev, dec, gather_to_root):
     import ctcext_amd
     from ctcext_amd import _lib
     B, T, C, W, P, merge, blank = cfg
-    rng = np.random.default_rng(20251015)
-    xg = rng.standard_normal((T, B, C), dtype=np.float32)
+
+    def shard(lo, nb):
+        # items [lo, lo + nb) of the global batch (seed 20251015): at N=1 the
+        # resident x is that batch; otherwise drawn as make_inputs draws it
+        # (past HOST_GEN_LIMIT on the device), never a second host copy of it
+        if world == 1:
+            return x[:, lo:lo + nb].contiguous()
+        _, xg, _, _ = make_inputs(cfg, 0, dev)
+        xs = xg[:, lo:lo + nb].contiguous()
+        del xg
+        return xs
+
     def run(xs, nb, outputs, gather):
         slt = torch.full((nb,), T, dtype=torch.int32, device=dev)
         out = ctcext_amd.ctc_ext_beam_search_decoder(xs, slt, W, P, merge_repeated=merge, blank_index=blank,
@@ -167,7 +177,7 @@ def strong_scaling(args, cfg, world, rank, dev, dec, gather_to_root):
     steps = max(2, min(args.steps, 5))
     if world > 1:
         nb = B // world
-        xs = torch.as_tensor(np.ascontiguousarray(xg[:, rank * nb:(rank + 1) * nb]), device=dev)
+        xs = shard(rank * nb, nb)
         run(xs, nb, "device", True)
         torch.cuda.synchronize()
         dist.barrier()
@@ -190,7 +200,7 @@ def strong_scaling(args, cfg, world, rank, dev, dec, gather_to_root):
         nb = B // n
         if nb == 0:
             continue
-        xs = torch.as_tensor(np.ascontiguousarray(xg[:, :nb]), device=dev)
+        xs = shard(0, nb)
         run(xs, nb, "device", False)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -381,7 +391,7 @@ def main():
         res["host_io"] = {"frames_per_s": int(sl_np.sum()) / io_s, "ms_per_step": 1e3 * io_s,
                           "steps": n_io, "what": "host numpy logits in, host numpy outputs out (PCIe both ways)"}
     if not args.no_strong and not args.seq_len and not args.batch_per_gpu and B % 2 == 0:
-        res["strong"] = strong_scaling(args, cfg, world, rank, dev, dec, gather_to_root)
+        res["strong"] = strong_scaling(args, cfg, world, rank, dev, dec, gather_to_root, x)
     if rank == 0 and world == 1 and not args.no_cpu:
         share, info = cpu_share()
         nw = args.cpu_workers or share

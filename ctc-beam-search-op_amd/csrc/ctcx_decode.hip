@@ -3057,7 +3057,8 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     for (int k = lane; k < 2 * W; k += 64) rg.st[k] = -1;   // no stamp yet
   Rec* const rstream = prm.rec + b * prm.Tmax * W;   // item b's record stream (ring)
   int32_t* const foff = prm.foff ? prm.foff + b * prm.Tmax : nullptr;
-  int flushed = 0, nflush = 0, nrec = 0;   // first frame not yet in HBM, flushes, records written
+  int flushed = 0, nflush = 0, nrec = 0;   // first frame not yet in HBM, flushes, ring stream cursor
+  int64_t nrec_all = 0;                    // records written without the ring (T * W can pass 2^31)
 
   // Reset(): root with newp.total = newp.blank = 0 (decoder.h:213-227)
   int buf = 0;
@@ -3298,7 +3299,7 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
       if (pp >= 0 && (!dup || cx.alias[k] == k))
         cx.sib[k] = __hip_atomic_exchange(&cx.head[pp], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    if (R == 0) nrec += n;
+    if (R == 0) nrec_all += n;
     else if (t - flushed + 1 == R) {   // the ring is full: write its older half
       ring_flush<KM>(rg, rstream, foff, t, flushed, flushed + R / 2 - 1, nullptr, 0, nflush, nrec);
       flushed += R / 2;
@@ -3340,8 +3341,8 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     io.dup_frames = dup_frames;
     io.why_nonfinite = why_nf;
     io.why_fill = why_fill;
-    io.records = nrec;
-    io.pad[0] = io.pad[1] = 0;
+    io.records = R > 0 ? (int64_t)nrec : nrec_all;
+    io.pad = 0;
     prm.item[b] = io;
   }
 }
@@ -3366,12 +3367,14 @@ constexpr int kNormTile = 64;
 template <typename T>
 __global__ __launch_bounds__(64) void ctcx_row_norm(const T* __restrict__ x, const int32_t* seq_len,
                                                    T* __restrict__ norm, int64_t Tmax, int64_t B, int64_t C,
-                                                   int64_t xstride) {
+                                                   int64_t xstride, const char* __restrict__ prep) {
   __shared__ T tile[64][kNormTile + 1];   // [row in wave][class in tile], padded: conflict-free row reads
+  __shared__ uint64_t etab[32];           // expf's 2^(i/32) table: the lanes' indices diverge
   const int lane = threadIdx.x;
   const int64_t rows = Tmax * B;
   const int64_t r0 = (int64_t)blockIdx.x * 64;
   const int64_t row = r0 + lane;
+  if (lane < 32) etab[lane] = gm::exp2f_tab(lane);   // read after the first tile's barrier
   bool valid = false;
   int64_t off = 0;   // this lane's row, in elements of x
   if (row < rows) {
@@ -3381,32 +3384,52 @@ __global__ __launch_bounds__(64) void ctcx_row_norm(const T* __restrict__ x, con
   }
   const uint64_t vmask = __ballot(valid);
   if (vmask == 0) return;
+  // the row maximum: from the pre-pass's header (ctcx_row_facts, C > 64) when
+  // the row holds no NaN / +inf (max is then order-free); otherwise pass 0
+  // takes it in class order, as the reference's maxCoeff loop does
   T m = T(0), s = T(0);
-  for (int pass = 0; pass < 2; ++pass) {
+  bool known = false;
+  if (prep != nullptr && valid) {
+    const RowHdr<T> h = *(const RowHdr<T>*)(prep + row * (int64_t)prep_row_bytes(C, (int)sizeof(T)));
+    if (!h.bad) { m = h.xmax; known = true; }
+  }
+  const bool pass0 = __ballot(valid && !known) != 0ull;
+  auto load = [&](T (&v)[64], int64_t c0) {
+    // row rr of the tile: one load per lane, sizeof(T) * nc contiguous bytes
+    // (an invalid row reads x's first row instead and is never used)
+    const int nc = (int)(C - c0 < kNormTile ? C - c0 : kNormTile);
+    const int col = lane < nc ? (int)c0 + lane : 0;
+#pragma unroll
+    for (int rr = 0; rr < 64; ++rr) {
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)off, rr);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)off >> 32), rr);
+      v[rr] = x[(int64_t)(((uint64_t)hi << 32) | lo) + col];
+    }
+  };
+  T v[64];
+  for (int pass = pass0 ? 0 : 1; pass < 2; ++pass) {
+    // the tile is (re)loaded unless C <= 64 and pass 0 left it in LDS; the
+    // next tile's loads are issued before this tile's sums (software pipeline)
+    const bool reload = pass == 0 || C > kNormTile || !pass0;
+    if (reload) load(v, 0);
     for (int64_t c0 = 0; c0 < C; c0 += kNormTile) {
       const int nc = (int)(C - c0 < kNormTile ? C - c0 : kNormTile);
-      if (pass == 0 || C > kNormTile) {
+      if (reload) {
         __syncthreads();
-        // row rr of the tile: one load per lane, sizeof(T) * nc contiguous
-        // bytes; all 64 loads are issued before the first LDS write (an
-        // invalid row reads x's first row instead and is never used)
-        T v[64];
-        const int col = lane < nc ? (int)c0 + lane : 0;
-#pragma unroll
-        for (int rr = 0; rr < 64; ++rr) {
-          const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)off, rr);
-          const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)off >> 32), rr);
-          v[rr] = x[(int64_t)(((uint64_t)hi << 32) | lo) + col];
-        }
 #pragma unroll
         for (int rr = 0; rr < 64; ++rr) tile[rr][lane] = v[rr];
         __syncthreads();
+        if (c0 + kNormTile < C) load(v, c0 + kNormTile);
       }
       if (valid) {
         if (pass == 0) {
-          int j = 0;
-          if (c0 == 0) { m = tile[lane][0]; j = 1; }
-          for (; j < nc; ++j) { const T v = tile[lane][j]; m = (v > m) ? v : m; }
+          if (!known) {
+            int j = 0;
+            if (c0 == 0) { m = tile[lane][0]; j = 1; }
+            for (; j < nc; ++j) { const T e = tile[lane][j]; m = (e > m) ? e : m; }
+          }
+        } else if constexpr (sizeof(T) == 4) {
+          for (int j = 0; j < nc; ++j) s += gm::expf_t(tile[lane][j] - m, etab);
         } else {
           for (int j = 0; j < nc; ++j) s += norm_exp(tile[lane][j] - m);
         }
@@ -3646,6 +3669,182 @@ __global__ __launch_bounds__(64) void ctcx_row_prep(const T* __restrict__ x, con
     for (int j = 0; j < Ci; ++j) ssum += norm_exp(xr[j] - m);
   }
   if (lane == 0) norm[row] = m + norm_log(ssum);
+}
+
+// ---------------------------------------------------------------------------
+// ctcx_row_facts: ctcx_row_prep's row facts (RowHdr, block maxima, the top
+// set S) for float rows with C % 4 == 0 and C <= 1024 * NV, with the row in
+// registers instead of LDS: lane L holds classes 4 (64 u + L) + c of the row
+// (float4 loads, u < NV, c < 4), all NV loads in flight at once, and every
+// pass over the row (maxima, counts, S) runs on those registers.  A 64-class
+// block is one 16-lane DPP row of one u, so the block maxima are DPP row
+// reductions.  The normaliser is left to ctcx_row_norm (rows per lane, the
+// class-order sum spread over 64 rows at a time, the maximum taken from the
+// header written here): the one-lane class-order sum of ctcx_row_prep was the
+// bulk of its time.  Four rows per 256-thread block, one per wave.
+template <int NV>
+__global__ __launch_bounds__(256) void ctcx_row_facts(const float* __restrict__ x,
+                                                     const int32_t* __restrict__ seq_len, char* __restrict__ prep,
+                                                     int64_t rows, int64_t B, int C, int64_t xstride, int blank) {
+  __shared__ unsigned cks_all[4][kPrepCompact];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t row = (int64_t)blockIdx.x * 4 + wv;
+  if (row >= rows) return;   // wave-uniform, and no block barrier below
+  const int64_t t = row / B, b = row - t * B;
+  if (t >= seq_len[b]) return;
+  const float NI = -__builtin_inff(), PI = __builtin_inff();
+  const int C4 = C >> 2;
+  const float4* xr = (const float4*)(x + (t * xstride + b) * (int64_t)C);
+  char* pr = prep + row * (int64_t)prep_row_bytes(C, 4);
+  float* bm = (float*)(pr + prep_bmax_offset(4));
+  const int nblk = (C + 63) / 64;
+  // the row, then its keys: fkey of each non-blank class, 0 for the blank and
+  // the padding (fkey is order-preserving; 0 is the key of one NaN pattern
+  // only, and a row holding a NaN is decoded literally, without S)
+  unsigned k[NV][4];
+#pragma unroll
+  for (int u = 0; u < NV; ++u) {
+    const int q = 64 * u + lane;
+    float4 f = make_float4(NI, NI, NI, NI);
+    if (q < C4) f = xr[q];
+    k[u][0] = __float_as_uint(f.x); k[u][1] = __float_as_uint(f.y);
+    k[u][2] = __float_as_uint(f.z); k[u][3] = __float_as_uint(f.w);
+  }
+  // maximum, NaN / +inf, the block maxima (block 4 u + (lane >> 4) is the
+  // 16-lane DPP row of one u: its maximum lands on the row's lane 15)
+  float xmax = NI;
+  bool bad = false;
+#pragma unroll
+  for (int u = 0; u < NV; ++u) {
+    float lm = NI;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float v = __uint_as_float(k[u][c]);
+      bad |= (v != v) || (v == PI);
+      lm = v > lm ? v : lm;
+      const int cl = 4 * (64 * u + lane) + c;
+      k[u][c] = (64 * u + lane < C4 && cl != blank) ? fkey(v) : 0u;
+    }
+    xmax = lm > xmax ? lm : xmax;
+    float w;
+    w = dpp_f<0x111>(lm, NI); lm = w > lm ? w : lm;
+    w = dpp_f<0x112>(lm, NI); lm = w > lm ? w : lm;
+    w = dpp_f<0x114>(lm, NI); lm = w > lm ? w : lm;
+    w = dpp_f<0x118>(lm, NI); lm = w > lm ? w : lm;
+    const int kb = 4 * u + (lane >> 4);
+    if ((lane & 15) == 15 && 64 * u < C4 && kb < nblk) bm[kb] = lm;
+  }
+  RowHdr<float> h;
+  h.xmax = wave_max_dpp(xmax);
+  h.bad = __ballot(bad) != 0ull;
+  const int K = kTopK;
+  // |{non-blank classes with key >= tau}| for tau >= 1
+  auto cnt_ge = [&](unsigned tau) __attribute__((always_inline)) {
+    int n = 0;
+#pragma unroll
+    for (int u = 0; u < NV; ++u)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) n += k[u][c] >= tau ? 1 : 0;
+    return uni(wave_sum_dpp(n));
+  };
+  auto bisect = [&](uint64_t& lo, uint64_t& hi) __attribute__((always_inline)) {
+    while (hi - lo > 1) {
+      const uint64_t mid = (lo + hi) >> 1;
+      const int c = cnt_ge((unsigned)mid);
+      if (c <= K) hi = mid;
+      else lo = mid;
+      if (c == K) break;
+    }
+  };
+  uint64_t lo = 0, hi = 1;   // tau in (lo, hi]: cnt(lo) > K >= cnt(hi); C - 1 <= K: tau = 1, all of them
+  if (C - 1 > K) {
+    hi = (uint64_t)fkey(h.xmax) + 1ull;   // cnt(hi) = 0
+    // the smallest lane maximum km: one key per lane at or above it, so
+    // cnt(km) >= 64 when every lane holds a label (C >= 256; else km = 0)
+    unsigned lk = 0u;
+#pragma unroll
+    for (int u = 0; u < NV; ++u)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) lk = k[u][c] > lk ? k[u][c] : lk;
+    const unsigned km = (unsigned)uni((int)wave_min_dpp(lk));
+    const int ckm = km > 0u ? cnt_ge(km) : C - 1;
+    if (km > 0u && ckm == K) {
+      lo = km - 1;   // exactly the K largest: tau = km
+      hi = km;
+    } else if (km > 0u && ckm <= kPrepCompact) {
+      // every key >= km into a compact list, then bisect in registers
+      lo = km;
+      unsigned* cks = cks_all[wv];
+      int n = 0;
+#pragma unroll
+      for (int u = 0; u < NV; ++u)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const bool in = k[u][c] >= km;
+          const uint64_t mm = __ballot(in);
+          if (in) cks[n + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mm >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((unsigned)mm, 0u))] = k[u][c];
+          n += __builtin_popcountll(mm);
+        }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      unsigned ck[kPrepCompact / 64];
+#pragma unroll
+      for (int q = 0; q < kPrepCompact / 64; ++q) ck[q] = 64 * q + lane < n ? cks[64 * q + lane] : 0u;
+      while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) >> 1;
+        int c = 0;
+#pragma unroll
+        for (int q = 0; q < kPrepCompact / 64; ++q) c += ck[q] >= (unsigned)mid ? 1 : 0;
+        c = uni(wave_sum_dpp(c));
+        if (c <= K) hi = mid;
+        else lo = mid;
+        if (c == K) break;
+      }
+    } else {
+      if (km > 0u) lo = km;   // cnt(km) > K; else cnt(0) = C - 1 > K
+      bisect(lo, hi);
+    }
+  }
+  // S in label-index order (within a u, class order is (lane, c) order), and
+  // the largest key of a label outside it
+  const unsigned tau = (unsigned)hi;
+  uint2* top = (uint2*)(pr + prep_top_offset(C, 4));
+  unsigned ko = 0u;
+  int n = 0;
+  const uint64_t ltm = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int u = 0; u < NV; ++u) {
+    if (64 * u < C4) {   // uniform
+      bool in[4];
+      uint64_t mm[4];
+      int before = 0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        in[c] = k[u][c] >= tau;
+        if (!in[c]) ko = k[u][c] > ko ? k[u][c] : ko;
+        mm[c] = __ballot(in[c]);
+        before += __builtin_popcountll(mm[c] & ltm);
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (in[c]) {
+          const int cl = 4 * (64 * u + lane) + c;
+          const unsigned kv = k[u][c];
+          const unsigned bits = kv ^ ((kv >> 31) ? 0x80000000u : 0xFFFFFFFFu);   // fkey's inverse
+          top[n + before] = make_uint2(bits, (unsigned)(cl - (cl > blank ? 1 : 0)));
+          ++before;
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) n += __builtin_popcountll(mm[c]);
+    }
+  }
+  h.ns = n;
+  ko = (unsigned)uni((int)~wave_min_dpp(~ko));   // the wave's largest
+  h.xout = ko == 0u ? NI : __uint_as_float(ko ^ ((ko >> 31) ? 0x80000000u : 0xFFFFFFFFu));
+  if (lane == 0) *(RowHdr<float>*)pr = h;
 }
 
 // ---------------------------------------------------------------------------
@@ -3893,18 +4092,54 @@ int ring_frames(const DecodeParams<T>& p, int cus, int cap) {
   if ((int64_t)p.Tmax * p.W > 0x7fffffffLL) return 0;
   const size_t base = (decode_lds_bytes(wcap, p.C, (int)sizeof(T), scored) + 15) & ~(size_t)15;
   const size_t budget = (base > 80 * 1024 || p.B <= cus) ? kLdsBytes : 80 * 1024;
-  for (int r = cap; r >= 8; r >>= 1)
+  // the kernel addresses ring rows by t & (R - 1): R must be a power of two
+  if (cap < 8) return 0;
+  cap = 1 << (31 - __builtin_clz((unsigned)cap));
+  for (int r = cap; r >= 8; r >>= 1) {
+    // ring_flush's stamps are fp * 4096 + (step + 1), fp the flush count
+    // (<= Tmax / (R / 2) + 1): they must stay below INT32_MAX
+    if (((int64_t)p.Tmax / (r / 2) + 2) * 4096 > 0x7fffffffLL) continue;
     if (base + ring_lds_bytes(r, p.W) <= budget) return r;
+  }
   return 0;
 }
 template int ring_frames<float>(const DecodeParams<float>&, int, int);
 template int ring_frames<double>(const DecodeParams<double>&, int, int);
+
+template <int NV>
+static hipError_t launch_row_facts(const float* x, const int32_t* sl, char* prep, int64_t rows, int64_t B, int C,
+                                   int64_t xstride, int blank, hipStream_t s) {
+  hipLaunchKernelGGL((ctcx_row_facts<NV>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, x, sl, prep, rows, B,
+                     C, xstride, blank);
+  return hipGetLastError();
+}
 
 template <typename T>
 hipError_t launch_row_prep(const T* x, const int32_t* sl, char* prep, T* norm, int64_t T_, int64_t B, int64_t C,
                            int64_t xstride, int blank, hipStream_t s) {
   const int64_t rows = T_ * B;
   if (rows == 0 || C <= 64) return hipSuccess;
+  if constexpr (sizeof(T) == 4) {
+    // float rows of whole float4s (16-byte aligned): the register-resident
+    // row facts, then the rows-per-lane normaliser reading their maxima
+    if (C % 4 == 0 && ((uintptr_t)x & 15) == 0 && C <= 1024 * 32) {
+      const int c4 = (int)(C / 4);
+      hipError_t e;
+      if (c4 <= 64) e = launch_row_facts<1>(x, sl, prep, rows, B, (int)C, xstride, blank, s);
+      else if (c4 <= 128) e = launch_row_facts<2>(x, sl, prep, rows, B, (int)C, xstride, blank, s);
+      else if (c4 <= 256) e = launch_row_facts<4>(x, sl, prep, rows, B, (int)C, xstride, blank, s);
+      else if (c4 <= 512) e = launch_row_facts<8>(x, sl, prep, rows, B, (int)C, xstride, blank, s);
+      else if (c4 <= 768) e = launch_row_facts<12>(x, sl, prep, rows, B, (int)C, xstride, blank, s);
+      else if (c4 <= 1024) e = launch_row_facts<16>(x, sl, prep, rows, B, (int)C, xstride, blank, s);
+      else if (c4 <= 1280) e = launch_row_facts<20>(x, sl, prep, rows, B, (int)C, xstride, blank, s);
+      else if (c4 <= 1536) e = launch_row_facts<24>(x, sl, prep, rows, B, (int)C, xstride, blank, s);
+      else e = launch_row_facts<32>(x, sl, prep, rows, B, (int)C, xstride, blank, s);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(ctcx_row_norm<T>, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, s, x, sl, norm, T_, B,
+                         C, xstride, (const char*)prep);
+      return hipGetLastError();
+    }
+  }
   const size_t row_b = (size_t)C * sizeof(T);
   // the expf table, the row, then the compact key list
   const size_t lds = kPrepTabBytes + ((row_b + 15) & ~(size_t)15) + 4 * kPrepCompact;
@@ -3933,7 +4168,7 @@ hipError_t launch_row_norm(const T* x, const int32_t* sl, T* norm, int64_t T_, i
   const int64_t rows = T_ * B;
   if (rows == 0) return hipSuccess;
   hipLaunchKernelGGL(ctcx_row_norm<T>, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, s, x, sl, norm, T_, B, C,
-                     xstride);
+                     xstride, (const char*)nullptr);
   return hipGetLastError();
 }
 template hipError_t launch_row_norm<float>(const float*, const int32_t*, float*, int64_t, int64_t, int64_t, int64_t,

@@ -65,9 +65,10 @@ struct ItemOut {
   int32_t dup_frames;     // frames whose beam held one entry twice (-inf logits)
   int32_t why_nonfinite;  // literal replays caused by a non-finite logit or total
   int32_t why_fill;       // ... by the beam filling up mid-frame
-  int32_t records;        // records written to HBM (all of them without the record ring)
-  int32_t pad[2];
+  int32_t pad;
+  int64_t records;        // records written to HBM (all of them without the record ring; T * W can pass 2^31)
 };
+static_assert(sizeof(ItemOut) == 32, "ItemOut layout");
 
 // Large C (> 64): per-(t, b) row facts computed by the parallel pre-pass
 // ctcx_row_prep before the decode kernel, which would otherwise derive them

@@ -14,8 +14,12 @@ size-independent properties, where the CPU oracle would take hours:
   kernels.cc:68-90): decoding any contiguous shard gives exactly the rows the
   full batch gives, and repeated calls are bit-identical.
 
-Oracle parity at these shapes is covered on a few full-length items in
-test_gpu_parity.py (test_cfg3_full_length_parity, test_cfg2_full_length_parity).
+Oracle parity at these shapes is pinned on full-length items: the committed
+oracle fixtures tests/golden/full_length.json (cfg3 T=1500, cfg4 T=2000, cfg5
+T=3000 and the peaky distribution; test_gpu_parity.py::test_full_length_golden,
+and cfg4's items inside the whole B=1024 workload,
+test_gpu_sharded.py::test_cfg4_whole_workload_eight_shards), plus the live
+oracle at cfg2/cfg3 (test_cfg2_full_length_parity, test_cfg3_full_length_parity).
 """
 import numpy as np
 import pytest

@@ -127,6 +127,54 @@ def test_sharded_root_shard_empty(device_in):
     compare(one, oracle.decode(x, sl, 4, 1), 1)
 
 
+def test_cfg4_whole_workload_eight_shards():
+    """BASELINE.json cfg4 as one call: B=1024, T=2000, C=1000 (BPE vocab),
+    beam_width=64 -- kernels.cc:68-90's batch loop over the whole global batch
+    -- through the sharded handle with eight shards (devices=[0]*8: eight
+    streams and workspaces on the one GPU of this box, the strided shard
+    copies and the peer-copy gather path; xGMI itself needs eight GPUs).
+    Checks: bit-identical to the one-device call; the full_length.json cfg4
+    items (oracle outputs at T=2000) placed at known batch positions -- across
+    the shard boundary at 127/128 and in the last shard -- come back
+    bit-exact; and the size-independent properties of test_gpu_properties."""
+    import json
+    from test_gpu_properties import _check_structure, _rows
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import make_fixtures_full
+    B, T, C, W, P = 1024, 2000, 1000, 64, 1
+    fixtures = json.load(open(os.path.join(ROOT, "tests", "golden", "full_length.json")))
+    g = torch.Generator(device="cuda")
+    g.manual_seed(4001)
+    x = torch.randn((T, B, C), generator=g, device="cuda", dtype=torch.float32)   # 8.2 GB
+    sl_np = np.random.default_rng(41).integers(T // 2, T + 1, size=B).astype(np.int32)
+    placed = {}   # batch position -> (fixture, item)
+    for name, pos in (("cfg4_T2000_B2", (127, 128)), ("cfg4_peaky_T2000", (1023,))):
+        fx = fixtures[name]
+        assert fx["case"][5:10] == [W, P, False, 0, -1], name
+        xf, slf = make_fixtures_full.inputs(fx["case"])
+        for item, b in enumerate(pos):
+            x[:, b] = torch.as_tensor(xf[:, item], device="cuda")
+            sl_np[b] = slf[item]
+            placed[b] = (fx, item)
+    sl = torch.as_tensor(sl_np, device="cuda")
+    kw = dict(merge_repeated=False, blank_index=0, blank_label=-1)
+    one = ctcext_amd.ctc_ext_beam_search_decoder(x, sl, W, P, **kw)
+    many = ctcext_amd.ctc_ext_beam_search_decoder(x, sl, W, P, devices=[0] * 8, **kw)
+    torch.cuda.synchronize()
+    assert ctcext_amd.get_decoder(tuple([0] * 8)).last_stats["n_devices"] == 8
+    del x
+    torch.cuda.empty_cache()
+    _same(many, one, P)
+    dec = _rows(many.decoded_indices[0], many.decoded_values[0], B)
+    ali = _rows(many.alignment_indices[0], many.alignment_values[0], B)
+    lp = to_numpy(many.log_probability)
+    for b, (fx, item) in placed.items():
+        assert dec[b] == fx["decoded"][item][0], b
+        assert ali[b] == fx["alignment"][item][0], b
+        assert lp[b, 0] == np.float32(float.fromhex(fx["log_probability_hex"][item][0])), b
+    _check_structure(many, sl_np, C, P, False)
+
+
 def _memory_probe():
     import psutil
     free, _ = torch.cuda.mem_get_info(0)
