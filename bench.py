@@ -39,14 +39,14 @@ CONFIGS = {
     "cfg5": (512, 3000, 5000, 256, 1, False, 0),
 }
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# Calibration of the CPU baseline (BASELINE.md "Calibration of the CPU baseline"): the oracle's
-# reference-cost mode ("port") timed in the build container on SURVEY.md 6's
-# cfg3-shape item (C=29, W=128, P=3, T=1500, merge) ran 81-104 frames/s per
-# core (median of 5 runs ~88) against the compiled reference's 189 frames/s
-# per core measured by the survey on the same container type.  The port is
-# therefore ~0.47x the reference's speed; the reference-equivalent CPU figure
-# is the port's divided by this ratio.
-PORT_OVER_REFERENCE = 0.47
+# Calibration of the CPU baseline (BASELINE.md "Calibration of the CPU
+# baseline", tools/cpu_calibrate.py): the oracle's reference-cost mode ("port")
+# timed in the build container on SURVEY.md 6's cfg3-shape item (C=29, W=128,
+# P=3, T=1500, merge), one cold call per fresh process as cpu_baseline runs it:
+# median 156.9 frames/s per core against the compiled reference's 189 measured
+# by the survey on the same container type.  The reference-equivalent CPU
+# figure is the port's divided by this ratio.
+PORT_OVER_REFERENCE = 0.83
 
 
 HOST_GEN_LIMIT = 4 << 30   # logits above 4 GiB (cfg5: 30.7 GB) are drawn on the device

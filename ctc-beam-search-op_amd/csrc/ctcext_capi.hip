@@ -571,6 +571,8 @@ static int run_decode(ctcext_decoder* d, const ctcext_decode_args* a, const std:
     d->stats.duplicate_frames += io[b].dup_frames;
     d->stats.records_written += io[b].records;
   }
+  for (int64_t b = 0; b < B; ++b)
+    if (io[b].pad != 0) return fail(CTCEXT_INTERNAL, "decode kernel: a helper-wave hand-over wait timed out");
   // TopPaths (decoder.h:240-243) fails on the first item with too few leaves
   for (int64_t b = 0; b < B; ++b)
     if (io[b].n_leaves < P) return fail(CTCEXT_INVALID_ARGUMENT, "Less leaves in the beam search than requested.");

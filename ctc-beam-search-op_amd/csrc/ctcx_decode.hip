@@ -32,6 +32,7 @@
 //     189-199).  Such a frame is replayed from the untouched frame-start state.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "ctcx_kernels.h"
 #include "ctcx_topn.h"
@@ -243,6 +244,7 @@ struct Ctx {
   int rbad, rns;
   int W, C, blank, enc, hts, wcap;
   int hdum;            // he index of lane 0's dummy store slot
+  int tabdead;         // HW kernels: a score-table wait gave up (never in a correct run)
 };
 
 // Per-64-label block maxima of the logit row, right after the row (large C).
@@ -1583,11 +1585,141 @@ __device__ __forceinline__ void cq_children(const Ctx<T>& cx, int buf, int nb, i
 }
 constexpr int kGatherWin = 8;   // kept 64-label windows per batch of row reads in the gather
 
-template <typename T, int RN, bool BIG, class SC>
+// ---------------------------------------------------------------------------
+// Helper wave (HW kernels: float, beams <= 128, C <= 64, the base scorer).
+// The decode workgroup has two waves on two SIMDs of the CU.  Wave 0 decodes
+// (the TopN pushes and the sort_heap extract: the frame's dependent chain);
+// wave 1 takes the frame's order-independent work off it:
+//   * the roll, the recursion and the commit are split over both waves;
+//   * during the grow, wave 1 scores the frame's offers ahead of wave 0 into
+//     a ring of chunk slots in LDS (the score table): chunk c holds offers
+//     [64c, 64c + 64) in (branch, label index) order, per lane its score, its
+//     branch's total, the packed (branch, label, label index, branch child),
+//     and the child's label-ending alignment candidate (value, back-pointer).
+//     All of it depends only on the frame-start state (branch arrays, child
+//     lists, the row), which nothing changes during the grow.  What events
+//     change -- a branch deactivated, a branch child evicted -- wave 0 reads
+//     itself (bst) when it takes a window's two chunks.
+// Hand-over: wave 1 publishes its chunk count (hready, a release store after
+// the slot's writes), wave 0 its consumed count (dcons, after the slot's
+// reads are issued: one wave's LDS operations execute in order) and, when the
+// grow ends, gdone; a full ring or an unpublished chunk is waited out with
+// s_sleep.  Every wait is bounded (a bound hit never happens in a correct run;
+// it ends the wait instead of hanging the CU).
+// A barrier for code only wave 0 runs in HW kernels (one wave: its LDS
+// operations execute in order, so a compiler fence is enough), else the
+// workgroup barrier.
+template <bool HW>
+__device__ __forceinline__ void wsync() {
+  if constexpr (HW) {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  } else {
+    __syncthreads();
+  }
+}
+constexpr int kTabSlots = 16;          // chunk slots in the ring
+constexpr int kSpinCap = 1 << 16;      // s_sleep(1) rounds before a wait gives up (~4 ms)
+struct Tab {
+  CTCX_LDS u32x4* a;    // [slot][lane]: score, branch total, packed, candidate back-pointer
+  CTCX_LDS float* p;    // [slot][lane]: candidate value
+};
+__host__ __device__ inline size_t tab_lds_bytes() { return (size_t)kTabSlots * 64 * 20; }
+__device__ __forceinline__ Tab tab_carve(CTCX_LDS char* p) {
+  Tab t;
+  t.a = (CTCX_LDS u32x4*)p;
+  t.p = (CTCX_LDS float*)(p + (size_t)kTabSlots * 64 * 16);
+  return t;
+}
+// control words in misc[8..11]; kCtlDead (sticky for the kernel): a wait gave
+// up, every later wait returns at once, and the item reports it (ItemOut.pad)
+constexpr int kCtlReady = 8, kCtlCons = 9, kCtlDone = 10, kCtlDead = 11;
+__device__ __forceinline__ int ctl_ld(CTCX_LDS int* m, int k) {
+  return uni(__hip_atomic_load(&m[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+// packed: branch (bits 0-6), label (7-12), label index (13-18), branch child + 1 (19-26), valid (27)
+__device__ __forceinline__ unsigned tab_pack(int i, int l, int li, int cw, bool v) {
+  return (unsigned)i | ((unsigned)l << 7) | ((unsigned)li << 13) | ((unsigned)(cw + 1) << 19) | (v ? 1u << 27 : 0u);
+}
+
+template <typename T>
+__device__ __forceinline__ void help_score_chunks(const Ctx<T>& cx, Tab tb, int buf, int nb, T norm) {
+  static_assert(sizeof(T) == 4, "the score table holds float rows");
+  const int lane = threadIdx.x & 63;
+  const T NI = ninf<T>();
+  const int Cm1 = cx.C - 1, blank = cx.blank;
+  const float rcp = 1.0f / (float)Cm1;
+  const int nch = (nb * Cm1 + 63) >> 6;
+  CTCX_LDS int* m = cx.misc;
+  if (ctl_ld(m, kCtlDead) != 0) return;
+  for (int c = 0; c < nch; ++c) {
+    for (int spin = 0;; ++spin) {   // the grow still running, and a free slot
+      if (ctl_ld(m, kCtlDone) != 0) return;
+      if (spin > kSpinCap) {
+        __hip_atomic_store(&m[kCtlDead], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return;
+      }
+      const int cons = ctl_ld(m, kCtlCons);
+      c = c > cons ? c : cons;   // chunks wave 0 has passed are never read
+      if (c < cons + kTabSlots) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (c >= nch) return;
+    const int o = 64 * c + lane;
+    int q = (int)((float)o * rcp);
+    q -= (q * Cm1 > o) ? 1 : 0;
+    q += ((q + 1) * Cm1 <= o) ? 1 : 0;
+    const bool v = q < nb;
+    const int i = v ? q : 0;
+    const int li = v ? o - q * Cm1 : 0;
+    const int l = li + (li >= blank ? 1 : 0);
+    const int bl = sel(cx.lab, buf)[i];
+    const int bflg = sel(cx.flg, buf)[i];
+    const T bt = sel(cx.ot, buf)[i];
+    const T bob = sel(cx.ob, buf)[i];
+    const int hd = cx.head[i];
+    const T bcb = sel(cx.cb, buf)[i], bcn = sel(cx.cn, buf)[i];
+    const T xl = cx.row[l];
+    const T p = xl - norm;
+    const T sc = p + ((l == bl) ? bob : bt);
+    // the branch child the offer re-offers (GetChild finds it), if any
+    int cw = -1;
+    for (int k = v ? hd : -1; __ballot(k >= 0);) {
+      int nk = -1;
+      if (k >= 0) {
+        const int lk = sel(cx.lab, buf)[k];
+        const int sk = cx.sib[k];
+        if (lk == l) cw = k;
+        else nk = sk;
+      }
+      k = nk;
+    }
+    const bool recv_fresh = cw >= 0 ? (sel(cx.ot, buf)[cw] == NI) : true;
+    const T rs_blank = ((bflg & F_ROOT) && recv_fresh) ? T(0) : NI;
+    Best<T> cd{T(0), kBpNone, false};
+    cd.push(((bflg & F_HB) ? bcb : rs_blank) + p, (bflg & F_HB) ? (((uint32_t)i << 1) | 0u) : kBpRestart);
+    if (l != bl) cd.push(((bflg & F_HN) ? bcn : NI) + p, (bflg & F_HN) ? (((uint32_t)i << 1) | 1u) : kBpRestart);
+    const int slot = (c % kTabSlots) * 64 + lane;
+    u32x4 e;
+    e.x = __builtin_bit_cast(unsigned, (float)sc);
+    e.y = __builtin_bit_cast(unsigned, (float)bt);
+    e.z = tab_pack(i, l, li, cw, v);
+    e.w = cd.bp;
+    tb.a[slot] = e;
+    tb.p[slot] = (float)cd.p;
+    __hip_atomic_store(&m[kCtlReady], c + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
+
+template <typename T, int RN, bool BIG, class SC, bool HW>
 __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, bool last, int P, int* n_out,
-                          int* n_leaves, uint64_t* pc) {
+                          int* n_leaves, uint64_t* pc, Tab tb) {
   uint64_t ts0 = pc ? __builtin_amdgcn_s_memtime() : 0;
-  const int lane = threadIdx.x;
+  // HW: both waves run up to the recursion, then wave 1 becomes the helper;
+  // wave 0 (threadIdx.x == lane) runs the rest
+  const int lane = threadIdx.x & 63;
+  constexpr int NT = HW ? 128 : 64;
+  const int tid = threadIdx.x;
   const T NI = ninf<T>();
   const int W = cx.W;
   const int C = cx.C;
@@ -1616,24 +1748,31 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
   // every offer's score p + base computed the reference's way
   const T pmax = xmax - norm;
 
-  // roll (decoder.h:87-92) + recursion (decoder.h:95-143), lanes over branches
-  for (int i = lane; i < nb; i += 64) {
+  // roll (decoder.h:87-92) + recursion (decoder.h:95-143), threads over branches
+  for (int i = tid; i < nb; i += NT) {
     cx.et[i] = sel(cx.ot, buf)[i]; cx.eb[i] = sel(cx.ob, buf)[i]; cx.el[i] = sel(cx.ol, buf)[i];
     cx.eflg[i] = 0;
     cx.bst[i] = 0;
     cx.bloom[i] = 0;
   }
   __syncthreads();
-  for (int i = lane; i < nb; i += 64) recurse_branch<T, SC>(cx, buf, i, i, norm, false);
+  for (int i = tid; i < nb; i += NT) recurse_branch<T, SC>(cx, buf, i, i, norm, false);
   __syncthreads();
   bool nonfinite = false;
-  for (int i = lane; i < nb; i += 64) {
+  for (int i = lane; i < nb; i += 64) {   // (HW: each wave tests every branch, so both decide alike)
     const T v = cx.et[i];
     nonfinite |= !(v > NI && v < pinf<T>());
-    he_st(he, i + 1, HE<T>{v, i});     // leaves_.push(b) in branch order
+    if (!HW || tid < 64) he_st(he, i + 1, HE<T>{v, i});     // leaves_.push(b) in branch order
   }
   if (__ballot(nonfinite)) return 1;
-  __syncthreads();
+  if constexpr (HW) {
+    if (tid >= 64) {
+      help_score_chunks<T>(cx, tb, buf, nb, norm);
+      return 0;   // the kernel takes wave 0's result
+    }
+  } else {
+    __syncthreads();
+  }
 
   uint64_t ts1 = pc ? __builtin_amdgcn_s_memtime() : 0;
   if (pc) pc[1] += ts1 - ts0;
@@ -1694,6 +1833,193 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
         // the windows run as one loop of their own (each window ends with the
         // grow's state in registers; the generic chunk path's loop-carried
         // state stays out of it): from here on the frame's grow is windows only
+#define CTCX_WIN_HALF(H, O)                                                                                       \
+          for (;;) {                                                                                                \
+            int k, cnt = 0;                                                                                         \
+            fv = uni(fv); fs = uni(fs); nfree = uni(nfree); nv = uni(nv);                                           \
+            const uint64_t ta = pc ? __builtin_amdgcn_s_memtime() : 0;                                              \
+            const int est = heap_events2_f32<H == 0>(sw[H], cw[H], slw[H] - 64 * H, cw[O], slw[O] - 64 * H,      \
+                                                     geo.anc, geo.req, aj,                                         \
+                                                     al, ar, dum, mys[H], mys[O], evr, batw[H], batw[O], NCw[H],   \
+                                                     RBw[H], RBw[O], donew[H], LBw[H], LBw[O], fv, fs, nfree, nv,  \
+                                                     uni(nb), 64 * H, k, cnt);                                     \
+            if (pc) { pc[13] += __builtin_amdgcn_s_memtime() - ta; pc[6] += uni(cnt); pc[12] += 1; }             \
+            if (est == 0) break;                                                                                    \
+            k = uni(k);                                                                                             \
+            const uint64_t gtM = __ballot(sw[H] > fv);                                                             \
+            const uint64_t m = ((gtM & NCw[H]) | RBw[H]) & ~donew[H];                                              \
+            if ((__ballot(!(bt[H] > batw[H])) >> k) & 1ull) {                                                      \
+              const int ksl = bcast(slw[H], k);                                                                     \
+              const uint64_t km0 = lowmask(ksl), km1 = ksl > 64 ? lowmask(ksl - 64) : 0ull;                        \
+              NCw[0] &= km0; LBw[0] &= km0; RBw[0] &= km0;                                                          \
+              NCw[1] &= km1; LBw[1] &= km1; RBw[1] &= km1;                                                          \
+              stop = true;                                                                                          \
+              continue;                                                                                             \
+            }                                                                                                       \
+            donew[H] = m ^ (m - 1ull);                                                                              \
+            const int kc = bcast(cw[H], k);                                                                         \
+            if (!((gtM >> k) & 1ull)) {                                                                             \
+              evr = writelane(evr, kc | kDeactRec, nv);                                                             \
+              nv += 1;                                                                                              \
+              const uint64_t dm0 = ~__ballot(wi[0] == kc), dm1 = ~__ballot(wi[1] == kc);                            \
+              NCw[0] &= dm0; LBw[0] &= dm0; RBw[0] &= dm0;                                                          \
+              NCw[1] &= dm1; LBw[1] &= dm1; RBw[1] &= dm1;                                                          \
+              continue;                                                                                             \
+            }                                                                                                       \
+            if (fs < nb) {                                                                                          \
+              evr = writelane(evr, fs, nv);                                                                         \
+              nv += 1;                                                                                              \
+              RBw[0] |= LBw[0] & __ballot(cw[0] == fs);                                                             \
+              RBw[1] |= LBw[1] & __ballot(cw[1] == fs);                                                             \
+            }                                                                                                       \
+            const T k_s = bcast(sw[H], k);                                                                          \
+            mys[0] = (mys[0] == fs) ? -1 : mys[0];                                                                  \
+            mys[1] = (mys[1] == fs) ? -1 : mys[1];                                                                  \
+            mys[H] = __builtin_amdgcn_inverse_ballot_w64(1ull << k) ? kc : mys[H];                                 \
+            HE<T> pL, pR;                                                                                           \
+            pairs_m(he, geo, pL, pR);                                                                               \
+            T c0;                                                                                                   \
+            int s0;                                                                                                 \
+            bool keep;                                                                                              \
+            push_m<T>(he, geo, k_s, kc, pL, pR, c0, s0, keep);                                                      \
+            fv = keep ? k_s : c0;                                                                                   \
+            fs = keep ? kc : s0;                                                                                    \
+            const int kp = k + 64 * H;                                                                              \
+            batw[0] = (slw[0] > kp) ? fv : batw[0];                                                                 \
+            batw[1] = (slw[1] > kp) ? fv : batw[1];                                                                 \
+          }
+        if constexpr (HW) {
+        const int nch = (nb * Cm1 + 63) >> 6;   // the frame's chunks
+        int ch = (i0 * Cm1 + li0) >> 6;
+        // the chunks before this one went by the generic path: their slots are free
+        __hip_atomic_store(&cx.misc[kCtlCons], ch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        do {
+          const uint64_t tc0 = pc ? __builtin_amdgcn_s_memtime() : 0;
+          const bool turnw = (li0 == 0);
+          const int c = ch;   // the window's first chunk (the generic chunks before it were 64 offers each)
+          ch += 2;
+          i0 += q128;   // 128 offers on: (i0, li0) + (q128, r128), one carry
+          li0 += r128;
+          if (li0 >= Cm1) { li0 -= Cm1; ++i0; }
+          // the window's two chunks from the score table: the published
+          // count is read first, so the slot reads issued after it see every
+          // chunk it covers (one wave's LDS operations execute in order)
+          const int need = c + 2 < nch ? c + 2 : nch;
+          u32x4 ta[2];
+          float tpv[2];
+          for (int spin = 0;; ++spin) {
+            const int rdy = __hip_atomic_load(&cx.misc[kCtlReady], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __asm__ volatile("" ::: "memory");
+            const int s0 = (c % kTabSlots) * 64 + lane, s1 = ((c + 1) % kTabSlots) * 64 + lane;
+            ta[0] = tb.a[s0];
+            tpv[0] = tb.p[s0];
+            ta[1] = tb.a[s1];
+            tpv[1] = tb.p[s1];
+            if (uni(rdy) >= need || cx.tabdead) break;
+            if (spin > kSpinCap) {   // never in a correct run: give up for the rest of the kernel
+              cx.tabdead = 1;
+              __hip_atomic_store(&cx.misc[kCtlDead], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+          __asm__ volatile("" ::: "memory");
+          __hip_atomic_store(&cx.misc[kCtlCons], c + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          int wi[2], wl[2], slw[2], cw[2], bsti[2], cst[2];
+          bool wv[2], wlive[2];
+          T sw[2], bt[2], batw[2];
+          Best<T> cdw[2];
+          uint64_t stM[2], wantM[2];
+  #pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const unsigned x = (h == 0 || c + 1 < nch) ? (unsigned)ta[h].z : 0u;
+            const unsigned a0 = ta[h].x, a1 = ta[h].y, a3 = ta[h].w;
+            wv[h] = ((x >> 27) & 1u) != 0u;
+            wi[h] = (int)(x & 127u);
+            wl[h] = (int)((x >> 7) & 63u);
+            const int wli = (int)((x >> 13) & 63u);
+            cw[h] = (int)((x >> 19) & 255u) - 1;
+            sw[h] = __builtin_bit_cast(float, a0);
+            bt[h] = __builtin_bit_cast(float, a1);
+            cdw[h] = Best<T>{(T)tpv[h], a3, true};
+            slw[h] = lane + 64 * h - wli;   // window position where the lane's branch turn starts
+            batw[h] = slw[h] > 0 ? bottom : NI;
+            stM[h] = __ballot(wv[h] && wli == 0 && lane + 64 * h != 0);
+          }
+          if (turnw && !(bcast(bt[0], 0) > bottom)) break;   // branch i0's turn: skipped, and all later
+          // what events change: the offer's branch deactivated, its branch child evicted
+  #pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            bsti[h] = cx.bst[wi[h]];
+            cst[h] = cx.bst[cw[h] >= 0 ? cw[h] : wi[h]];
+          }
+          uint64_t NCw[2], LBw[2], RBw[2], donew[2] = {0ull, 0ull};
+  #pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            wlive[h] = wv[h] && !(bsti[h] & S_DEACT);
+            const bool isbc = cw[h] >= 0;
+            const bool cev = isbc && (cst[h] & S_EVICT) != 0;
+            wantM[h] = __ballot(wlive[h] && (isbc ? cev : (sw[h] > bottom)));
+            const uint64_t liveM = __ballot(wlive[h]), isbm = __ballot(isbc);
+            NCw[h] = liveM & ~isbm;
+            LBw[h] = liveM & isbm;
+            RBw[h] = LBw[h] & __ballot(cev);
+          }
+          if (pc) pc[10] += __builtin_amdgcn_s_memtime() - tc0;
+          if (!(wantM[0] | wantM[1])) {
+            if ((stM[0] & ~__ballot(bt[0] > bottom)) | (stM[1] & ~__ballot(bt[1] > bottom))) break;
+            continue;
+          }
+          const uint64_t tc1 = pc ? __builtin_amdgcn_s_memtime() : 0;
+          if (pc) { pc[8] += tc1 - tc0; pc[11] += 1; }
+          int mys[2] = {-1, -1};
+          int evr = 0, nv = 0;
+          T fv = front.v;
+          int fs = front.s;
+          int nfree = nextfree;
+          const HeapM geo = heap_m(cx.hdum);
+          const unsigned heb = (unsigned)(uintptr_t)he;
+          const unsigned aj = heb + 8u * (unsigned)(lane + 1), al = heb + 8u * (unsigned)(2 * lane + 2);
+          const unsigned ar = al + 8u, dum = heb + 8u * (unsigned)(cx.hdum + lane);
+          // the events of half H (other half O); rare ones (re-offered branch
+          // children) are decided here, as in the chunk loop below
+          CTCX_WIN_HALF(0, 1)
+          donew[0] = ~0ull;   // the first half's offers are all behind
+          CTCX_WIN_HALF(1, 0)
+          front.v = fv;
+          front.s = fs;
+          bottom = fv;
+          nextfree = nfree;
+          // the turn continuing into the next window: skipped -> so is every later one
+          if ((__ballot(wv[1] && !(bt[1] > batw[1])) >> 63) & 1ull) stop = true;
+          const uint64_t q5 = pc ? __builtin_amdgcn_s_memtime() : 0;
+          if (lane < nv) {
+            const int rs = evr & ~kDeactRec;
+            if (evr & kDeactRec) {
+              __hip_atomic_fetch_or(&cx.bst[rs], S_DEACT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {
+              cx.et[rs] = NI; cx.eb[rs] = NI; cx.el[rs] = NI; cx.eflg[rs] = 0;
+              __hip_atomic_fetch_or(&cx.bst[rs], S_EVICT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              // (no bloom: the window path reads the events' effects from bst)
+            }
+          }
+  #pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int ms = mys[h];
+            if (ms >= 0) {
+              const bool isbc = cw[h] >= 0;
+              cx.et[ms] = sw[h]; cx.eb[ms] = NI; cx.el[ms] = sw[h];
+              cx.ecn[ms] = cdw[h].p; cx.ebpn[ms] = cdw[h].bp;
+              cx.eflg[ms] = F_HN;
+              cx.ekind[ms] = isbc ? ((uint32_t)cw[h] << 1) : (((uint32_t)wi[h] << 1) | 1u);
+              cx.elab[ms] = wl[h];
+              if (isbc) __hip_atomic_fetch_and(&cx.bst[cw[h]], ~S_EVICT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+          }
+          if (pc) pc[15] += __builtin_amdgcn_s_memtime() - q5;
+          if (pc) pc[9] += __builtin_amdgcn_s_memtime() - tc1;
+        } while (i0 < nb && !stop);
+        } else {
         do {
           // ---- HEAP_SORTED, C <= 64, float: 128-offer windows (two halves of
           // 64 lanes).  The same offer semantics as the 64-offer chunk below,
@@ -1815,65 +2141,9 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
           const unsigned ar = al + 8u, dum = heb + 8u * (unsigned)(cx.hdum + lane);
           // the events of half H (other half O); rare ones (re-offered branch
           // children) are decided here, as in the chunk loop below
-  #define CTCX_WIN_HALF(H, O)                                                                                       \
-          for (;;) {                                                                                                \
-            int k, cnt = 0;                                                                                         \
-            fv = uni(fv); fs = uni(fs); nfree = uni(nfree); nv = uni(nv);                                           \
-            const uint64_t ta = pc ? __builtin_amdgcn_s_memtime() : 0;                                              \
-            const int est = heap_events2_f32<H == 0>(sw[H], cw[H], slw[H] - 64 * H, cw[O], slw[O] - 64 * H,      \
-                                                     geo.anc, geo.req, aj,                                         \
-                                                     al, ar, dum, mys[H], mys[O], evr, batw[H], batw[O], NCw[H],   \
-                                                     RBw[H], RBw[O], donew[H], LBw[H], LBw[O], fv, fs, nfree, nv,  \
-                                                     uni(nb), 64 * H, k, cnt);                                     \
-            if (pc) { pc[13] += __builtin_amdgcn_s_memtime() - ta; pc[6] += uni(cnt); pc[12] += 1; }             \
-            if (est == 0) break;                                                                                    \
-            k = uni(k);                                                                                             \
-            const uint64_t gtM = __ballot(sw[H] > fv);                                                             \
-            const uint64_t m = ((gtM & NCw[H]) | RBw[H]) & ~donew[H];                                              \
-            if ((__ballot(!(bt[H] > batw[H])) >> k) & 1ull) {                                                      \
-              const int ksl = bcast(slw[H], k);                                                                     \
-              const uint64_t km0 = lowmask(ksl), km1 = ksl > 64 ? lowmask(ksl - 64) : 0ull;                        \
-              NCw[0] &= km0; LBw[0] &= km0; RBw[0] &= km0;                                                          \
-              NCw[1] &= km1; LBw[1] &= km1; RBw[1] &= km1;                                                          \
-              stop = true;                                                                                          \
-              continue;                                                                                             \
-            }                                                                                                       \
-            donew[H] = m ^ (m - 1ull);                                                                              \
-            const int kc = bcast(cw[H], k);                                                                         \
-            if (!((gtM >> k) & 1ull)) {                                                                             \
-              evr = writelane(evr, kc | kDeactRec, nv);                                                             \
-              nv += 1;                                                                                              \
-              const uint64_t dm0 = ~__ballot(wi[0] == kc), dm1 = ~__ballot(wi[1] == kc);                            \
-              NCw[0] &= dm0; LBw[0] &= dm0; RBw[0] &= dm0;                                                          \
-              NCw[1] &= dm1; LBw[1] &= dm1; RBw[1] &= dm1;                                                          \
-              continue;                                                                                             \
-            }                                                                                                       \
-            if (fs < nb) {                                                                                          \
-              evr = writelane(evr, fs, nv);                                                                         \
-              nv += 1;                                                                                              \
-              RBw[0] |= LBw[0] & __ballot(cw[0] == fs);                                                             \
-              RBw[1] |= LBw[1] & __ballot(cw[1] == fs);                                                             \
-            }                                                                                                       \
-            const T k_s = bcast(sw[H], k);                                                                          \
-            mys[0] = (mys[0] == fs) ? -1 : mys[0];                                                                  \
-            mys[1] = (mys[1] == fs) ? -1 : mys[1];                                                                  \
-            mys[H] = __builtin_amdgcn_inverse_ballot_w64(1ull << k) ? kc : mys[H];                                 \
-            HE<T> pL, pR;                                                                                           \
-            pairs_m(he, geo, pL, pR);                                                                               \
-            T c0;                                                                                                   \
-            int s0;                                                                                                 \
-            bool keep;                                                                                              \
-            push_m<T>(he, geo, k_s, kc, pL, pR, c0, s0, keep);                                                      \
-            fv = keep ? k_s : c0;                                                                                   \
-            fs = keep ? kc : s0;                                                                                    \
-            const int kp = k + 64 * H;                                                                              \
-            batw[0] = (slw[0] > kp) ? fv : batw[0];                                                                 \
-            batw[1] = (slw[1] > kp) ? fv : batw[1];                                                                 \
-          }
           CTCX_WIN_HALF(0, 1)
           donew[0] = ~0ull;   // the first half's offers are all behind
           CTCX_WIN_HALF(1, 0)
-  #undef CTCX_WIN_HALF
           front.v = fv;
           front.s = fs;
           bottom = fv;
@@ -1910,6 +2180,8 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
           if (pc) pc[15] += __builtin_amdgcn_s_memtime() - q5;
           if (pc) pc[9] += __builtin_amdgcn_s_memtime() - tc1;
         } while (i0 < nb && !stop);
+        }
+#undef CTCX_WIN_HALF
         break;
       }
     }
@@ -2581,6 +2853,8 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     if (pc) pc[9] += __builtin_amdgcn_s_memtime() - tc1;
   }
 
+  // the grow is over: the helper stops scoring
+  if constexpr (HW) __hip_atomic_store(&cx.misc[kCtlDone], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   if (BIG && cbr >= 0) cq_children(cx, buf, nb, cbr, -1);
   uint64_t ts2 = pc ? __builtin_amdgcn_s_memtime() : 0;
   if (pc) pc[2] += ts2 - ts1;
@@ -2596,7 +2870,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       for (int q = 0; q < size; ++q) lit_top_push(tp, cx.heap[q], gt);
       lit_top_extract(tp, gt);
     }
-    __syncthreads();
+    wsync<HW>();
   }
   // Extract() of the next frame (decoder.h:84): sort_heap, or std::sort
   int nout;
@@ -2705,14 +2979,14 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       lit_sort(cx.sorted, n, SlotGreater<T>{cx.et});
     }
   }
-  __syncthreads();
+  wsync<HW>();
   if (last && lane == 0) {
     // TopPaths slots -> sorted positions
     for (int q = 0; q < nout; ++q) cx.freel[cx.sorted[q]] = q;
     const int lim = (P < size) ? P : size;
     for (int q = 0; q < lim; ++q) cx.tops[q] = cx.freel[cx.tops[q]];
   }
-  __syncthreads();
+  wsync<HW>();
   if (pc) pc[3] += __builtin_amdgcn_s_memtime() - ts2;
   *n_out = nout;
   return 0;
@@ -3023,8 +3297,13 @@ __device__ void ring_flush(const Ring& g, Rec* out, int32_t* foff, int t_new, in
   __syncthreads();
 }
 
-template <typename T, int RN, int WC, bool BIG, class SC>
-__global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
+// HW: two waves per item (wave 1 the helper, see help_score_chunks); every
+// loop over positions below then runs over NT = 128 threads, and one-thread
+// work is thread 0's (wave 0, the decoding wave).
+template <typename T, int RN, int WC, bool BIG, class SC, bool HW>
+__global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T> prm) {
+  static_assert(!HW || (sizeof(T) == 4 && RN == 1 && WC == 128 && !BIG && !SC::kStateful), "HW kernels");
+  constexpr int NT = HW ? 128 : 64;
   Ctx<T> cx;
 #ifdef CTCX_GSTATE
   // global-state tier: the item's state in global memory (gstate_bytes), the
@@ -3037,7 +3316,9 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
 #endif
   cx.blank = prm.blank;
   cx.sctab = prm.scorer_tab;
-  const int lane = threadIdx.x;
+  cx.tabdead = 0;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
   const int64_t b = blockIdx.x;
   const int W = prm.W;
   const int C = (int)prm.C;
@@ -3053,6 +3334,11 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     rg = ring_carve((CTCX_LDS char*)lds + ((decode_lds_bytes(WC > 0 ? WC : W, C, (int)sizeof(T), SC::kStateful) +
                                             15) & ~(size_t)15), R, W);
 #endif
+  Tab tb{};
+#ifndef CTCX_GSTATE
+  if constexpr (HW)   // the score table after the decode layout (no record ring in HW kernels)
+    tb = tab_carve((CTCX_LDS char*)lds + ((decode_lds_bytes(WC, C, (int)sizeof(T), false) + 15) & ~(size_t)15));
+#endif
   if (R > 0)
     for (int k = lane; k < 2 * W; k += 64) rg.st[k] = -1;   // no stamp yet
   Rec* const rstream = prm.rec + b * prm.Tmax * W;   // item b's record stream (ring)
@@ -3062,8 +3348,9 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
 
   // Reset(): root with newp.total = newp.blank = 0 (decoder.h:213-227)
   int buf = 0;
-  if (lane < 32) cx.etab[lane] = gm::exp2f_tab(lane);
-  if (lane == 0) {
+  if (tid < 32) cx.etab[tid] = gm::exp2f_tab(tid);
+  if (tid == 0) {
+    cx.misc[kCtlDead] = 0;
     cx.lab[0][0] = -1; cx.par[0][0] = -1; cx.flg[0][0] = F_ROOT;
     cx.ot[0][0] = T(0); cx.ob[0][0] = T(0); cx.ol[0][0] = ninf<T>();
     cx.cb[0][0] = T(0); cx.cn[0][0] = T(0);
@@ -3099,8 +3386,10 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
 #ifdef CTCX_GSTATE
     cx.row = const_cast<T*>(xr);
 #else
-    for (int j = lane; j < C; j += 64) cx.row[j] = xr[j];
+    for (int j = tid; j < C; j += NT) cx.row[j] = xr[j];
 #endif
+    if constexpr (HW)
+      if (tid < 3) cx.misc[kCtlReady + tid] = 0;   // the helper's hand-over counters, per frame
     const T norm = prm.norm[(int64_t)t * B + b];
     if constexpr (BIG) {
       // the pre-pass record of row (t, b): header, block maxima, top set
@@ -3131,8 +3420,22 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     if (prof) pc[0] += t1 - t0;
 #ifndef CTCX_GSTATE   // the global-state tier replays every frame literally
     if (!prm.force_literal && !dup)
-      why = exact_step<T, RN, BIG, SC>(cx, buf, nb, norm, last, prm.P, &n, &nl_fast, prof ? pc : nullptr);
+      why = exact_step<T, RN, BIG, SC, HW>(cx, buf, nb, norm, last, prm.P, &n, &nl_fast, prof ? pc : nullptr, tb);
 #endif
+    if constexpr (HW) {
+      // wave 0's result for both waves; the helper stops if the grow ended
+      // early (a frame handed to the literal path)
+      if (tid == 0) {
+        __hip_atomic_store(&cx.misc[kCtlDone], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        cx.misc[4] = why;
+        cx.misc[5] = n;
+        cx.misc[6] = nl_fast;
+      }
+      __syncthreads();
+      why = uni(cx.misc[4]);
+      n = uni(cx.misc[5]);
+      nl_fast = uni(cx.misc[6]);
+    }
     __syncthreads();
     uint64_t t2 = prof ? __builtin_amdgcn_s_memtime() : 0;
     const bool ok = (why == 0);
@@ -3140,7 +3443,7 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     dup_frames += dup ? 1 : 0;
     bool dup_next = false;
     if (!ok) {
-      if (lane == 0) {
+      if (tid == 0) {
         int d2 = 0, nl = 0;
         misc[0] = literal_step<T, SC>(cx, buf, nb, norm, last, prm.P, dup, &d2, &nl);
         misc[1] = d2;
@@ -3166,19 +3469,19 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     // staged (unrolled, KM positions per lane) for a compile-time capacity, and
     // always in place (the LDS tier: W <= 512); plain loops otherwise (any W)
     constexpr bool STAGED = WC > 0 || INPLACE;
-    constexpr int KM = (WC > 0 ? WC : 512) / 64;
+    constexpr int KM = (WC > 0 ? WC : 512) / NT;   // positions per thread
     const int nx = INPLACE ? buf : buf ^ 1;
-    for (int i = lane; i < nb; i += 64) cx.newpos[i] = -1;
+    for (int i = tid; i < nb; i += NT) cx.newpos[i] = -1;
     __syncthreads();
     // (an entry the beam holds twice: its first position is the canonical one,
     // the one its children link to and the hash table maps to)
-    for (int k = lane; k < n; k += 64) {
+    for (int k = tid; k < n; k += NT) {
       const uint32_t kd = cx.ekind[cx.sorted[k]];
       if (!dup_next) cx.alias[k] = k;
       else if (cx.alias[k] != k) continue;
       if (!(kd & 1u)) cx.newpos[kd >> 1] = k;
     }
-    for (int q = lane; q < cx.hts; q += 64) cx.htab[q] = -1;
+    for (int q = tid; q < cx.hts; q += NT) cx.htab[q] = -1;
     __syncthreads();
     // One position k of the commit: the new prefix hash (phase 1), then the
     // parent position and flags (phase 2), then the writes.  In place (large
@@ -3256,45 +3559,45 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
 #pragma unroll
       for (int j = 0; j < KM; ++j) {
         nha[j] = nhb[j] = 0;
-        if (lane + 64 * j < n) hash_of(lane + 64 * j, nha[j], nhb[j]);
+        if (tid + NT * j < n) hash_of(tid + NT * j, nha[j], nhb[j]);
       }
       if constexpr (INPLACE) __syncthreads();
 #pragma unroll
       for (int j = 0; j < KM; ++j)
-        if (lane + 64 * j < n) put_hash(lane + 64 * j, nha[j], nhb[j]);
+        if (tid + NT * j < n) put_hash(tid + NT * j, nha[j], nhb[j]);
       __syncthreads();
       int npar[KM], nfl[KM];
 #pragma unroll
       for (int j = 0; j < KM; ++j) {
         npar[j] = -1;
         nfl[j] = 0;
-        if (lane + 64 * j < n) parent_of(lane + 64 * j, npar[j], nfl[j]);
+        if (tid + NT * j < n) parent_of(tid + NT * j, npar[j], nfl[j]);
       }
       if constexpr (INPLACE) __syncthreads();
 #pragma unroll
       for (int j = 0; j < KM; ++j)
-        if (lane + 64 * j < n) put_branch(lane + 64 * j, npar[j], nfl[j]);
+        if (tid + NT * j < n) put_branch(tid + NT * j, npar[j], nfl[j]);
     } else {
-      for (int k = lane; k < n; k += 64) {
+      for (int k = tid; k < n; k += NT) {
         uint64_t ha, hb;
         hash_of(k, ha, hb);
         put_hash(k, ha, hb);
       }
       __syncthreads();
-      for (int k = lane; k < n; k += 64) {
+      for (int k = tid; k < n; k += NT) {
         int parent, fl;
         parent_of(k, parent, fl);
         put_branch(k, parent, fl);
       }
     }
-    if (R > 0 && lane == 0) rg.rn[t & (R - 1)] = n;
+    if (R > 0 && tid == 0) rg.rn[t & (R - 1)] = n;
     __syncthreads();
     buf = nx;
     nb = n;
     dup = dup_next;
-    for (int k = lane; k < nb; k += 64) cx.head[k] = -1;
+    for (int k = tid; k < nb; k += NT) cx.head[k] = -1;
     __syncthreads();
-    for (int k = lane; k < nb; k += 64) {
+    for (int k = tid; k < nb; k += NT) {
       const int pp = sel(cx.par, buf)[k];
       if (pp >= 0 && (!dup || cx.alias[k] == k))
         cx.sib[k] = __hip_atomic_exchange(&cx.head[pp], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -3308,16 +3611,16 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     __syncthreads();
     if (prof) { pc[4] += __builtin_amdgcn_s_memtime() - t3; pc[7] += 1; }
   }
-  if (prof && lane == 0)
+  if (prof && tid == 0)
     for (int q = 0; q < kPhaseN; ++q) prm.prof[b * kPhaseN + q] = pc[q];
 
   // TopPaths outputs (decoder.h:230-261); with no frames the root is the leaf
-  if (sl == 0 && lane == 0) cx.tops[0] = 0;
+  if (sl == 0 && tid == 0) cx.tops[0] = 0;
   __syncthreads();
   const int np = (prm.P < n_leaves) ? prm.P : n_leaves;
   // the rest of the ring, walked from the TopPaths positions
   if (R > 0 && sl > 0) ring_flush<(WC > 0 ? WC : 512) / 64>(rg, rstream, foff, sl - 1, flushed, sl - 1, cx.tops, np, nflush, nrec);
-  for (int q = lane; q < prm.P; q += 64) {
+  for (int q = tid; q < prm.P; q += NT) {
     int pos = -1, kind = -1, opos = -1;
     T lp = T(0);
     if (q < np) {
@@ -3334,7 +3637,7 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     prm.top_kind[b * prm.P + q] = kind;
     prm.log_prob[b * prm.P + q] = lp;
   }
-  if (lane == 0) {
+  if (tid == 0) {
     ItemOut io;
     io.n_leaves = n_leaves;
     io.literal_steps = literal_steps;
@@ -3342,7 +3645,8 @@ __global__ __launch_bounds__(64) void ctcx_beam_decode(DecodeParams<T> prm) {
     io.why_nonfinite = why_nf;
     io.why_fill = why_fill;
     io.records = R > 0 ? (int64_t)nrec : nrec_all;
-    io.pad = 0;
+    // HW kernels: a hand-over wait that gave up (the host fails the call)
+    io.pad = HW ? __hip_atomic_load(&cx.misc[kCtlDead], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0;
     prm.item[b] = io;
   }
 }
@@ -3963,16 +4267,21 @@ __global__ __launch_bounds__(64) void ctcx_pack(PackParams pp) {
 // Launchers (called by the C-ABI layer).
 namespace ctcx {
 
-template <typename T, int RN, int WC, bool BIG, class SC>
+template <typename T, int RN, int WC, bool BIG, class SC, bool HW = false>
 hipError_t launch_decode_c(const DecodeParams<T>& p, hipStream_t s) {
   size_t lds = decode_lds_bytes(WC > 0 ? WC : p.W, p.C, (int)sizeof(T), SC::kStateful);
   if (p.ring > 0) lds = ((lds + 15) & ~(size_t)15) + ring_lds_bytes(p.ring, p.W);
+  if (HW) {
+    if (p.ring > 0) return hipErrorInvalidValue;   // (the dispatcher never asks: no ring in HW kernels)
+    lds = ((lds + 15) & ~(size_t)15) + tab_lds_bytes();
+  }
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)ctcx_beam_decode<T, RN, WC, BIG, SC>,
+    hipError_t e = hipFuncSetAttribute((const void*)ctcx_beam_decode<T, RN, WC, BIG, SC, HW>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((ctcx_beam_decode<T, RN, WC, BIG, SC>), dim3((unsigned)p.B), dim3(64), lds, s, p);
+  hipLaunchKernelGGL((ctcx_beam_decode<T, RN, WC, BIG, SC, HW>), dim3((unsigned)p.B), dim3(HW ? 128 : 64), lds, s,
+                     p);
   return hipGetLastError();
 }
 
@@ -4016,6 +4325,7 @@ hipError_t launch_decode_c(const DecodeParams<T>& p, hipStream_t s) {
 #define CTCX_IF_5(...)
 #define CTCX_IF_6(...)
 #define CTCX_IF_7(...)
+#define CTCX_IF_8(...)
 #if CTCX_PART == 1
 #undef CTCX_IF_1
 #define CTCX_IF_1(...) __VA_ARGS__
@@ -4037,6 +4347,9 @@ hipError_t launch_decode_c(const DecodeParams<T>& p, hipStream_t s) {
 #elif CTCX_PART == 7
 #undef CTCX_IF_7
 #define CTCX_IF_7(...) __VA_ARGS__
+#elif CTCX_PART == 8
+#undef CTCX_IF_8
+#define CTCX_IF_8(...) __VA_ARGS__
 #endif
 #define CTCX_IF_PART(P, ...) CTCX_IF_##P(__VA_ARGS__)
 #if CTCX_PART == 0
@@ -4048,6 +4361,14 @@ hipError_t launch_decode_c(const DecodeParams<T>& p, hipStream_t s) {
 #endif
 CTCX_DECODE_INSTANCES(CTCX_X)
 #undef CTCX_X
+// the two-wave (helper) kernel of the cfg2/cfg3 class, part 8
+#if CTCX_PART == 0
+extern template hipError_t launch_decode_c<float, 1, 128, false, BaseBeamScorer<float>, true>(
+    const DecodeParams<float>&, hipStream_t);
+#else
+CTCX_IF_PART(8, template hipError_t launch_decode_c<float, 1, 128, false, BaseBeamScorer<float>, true>(
+                    const DecodeParams<float>&, hipStream_t);)
+#endif
 
 #if CTCX_PART == 0
 // BIG (C > 64): the grow loop's branch/window skipping by row-block maxima is
@@ -4071,6 +4392,14 @@ hipError_t launch_decode(const DecodeParams<T>& p, hipStream_t s) {
     return launch_decode_r<T, 4, 0, SC>(p, s);
   }
   auto fits = [&](int wc) { return decode_lds_bytes(wc, p.C, (int)sizeof(T), false) <= kLdsBytes; };
+  if constexpr (sizeof(T) == 4) {
+    // float, beams <= 128, C <= 64, no record ring: the two-wave kernel
+    // (CTCEXT_HELPER=0, diagnostics: the one-wave kernel instead)
+    const char* hv = getenv("CTCEXT_HELPER");
+    if (p.W <= 128 && p.C <= 64 && p.ring == 0 && !(hv && hv[0] == '0') &&
+        ((decode_lds_bytes(128, p.C, 4, false) + 15) & ~(size_t)15) + tab_lds_bytes() <= kLdsBytes)
+      return launch_decode_c<float, 1, 128, false, BaseBeamScorer<float>, true>(p, s);
+  }
   if (p.W <= 128) return fits(128) ? launch_decode_r<T, 1, 128>(p, s) : launch_decode_r<T, 1, 0>(p, s);
   if (p.W <= 256) return fits(256) ? launch_decode_r<T, 2, 256>(p, s) : launch_decode_r<T, 2, 0>(p, s);
   return launch_decode_r<T, 4, 0>(p, s);
@@ -4209,7 +4538,7 @@ hipError_t launch_pack(const PackParams& pp, hipStream_t s) {
 namespace ctcx {
 template <typename T, class SC>
 static hipError_t launch_decode_gs_t(const DecodeParams<T>& p, hipStream_t s) {
-  hipLaunchKernelGGL((ctcx_beam_decode<T, 1, 0, false, SC>), dim3((unsigned)p.B), dim3(64), 0, s, p);
+  hipLaunchKernelGGL((ctcx_beam_decode<T, 1, 0, false, SC, false>), dim3((unsigned)p.B), dim3(64), 0, s, p);
   return hipGetLastError();
 }
 }  // namespace ctcx

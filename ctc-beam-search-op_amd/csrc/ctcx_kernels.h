@@ -65,7 +65,7 @@ struct ItemOut {
   int32_t dup_frames;     // frames whose beam held one entry twice (-inf logits)
   int32_t why_nonfinite;  // literal replays caused by a non-finite logit or total
   int32_t why_fill;       // ... by the beam filling up mid-frame
-  int32_t pad;
+  int32_t pad;            // two-wave kernels: nonzero if a helper hand-over wait gave up
   int64_t records;        // records written to HBM (all of them without the record ring; T * W can pass 2^31)
 };
 static_assert(sizeof(ItemOut) == 32, "ItemOut layout");
