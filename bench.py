@@ -355,9 +355,11 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "ctcx_beam_decode", "kernel_ms": kavg,
                      "algorithmic_bytes_per_launch": abytes,
-                     # beam records the decode kernel wrote to HBM (8 B each; with the
-                     # LDS record ring only those the traceback can reach)
-                     "record_ring_frames": st["ring_frames"], "records_written": st["records_written"]},
+                     # beam records the decode kernel wrote to HBM (record_bytes each:
+                     # 4 in the two-wave kernel; with the LDS record ring only those
+                     # the traceback can reach)
+                     "record_ring_frames": st["ring_frames"], "records_written": st["records_written"],
+                     "record_bytes": st["record_bytes"]},
         "literal_frames_per_step": lit / max(args.steps, 1),
         "lib_sha16": lib_hash(),
         "what": ("one decode call: device logits in, int64 SparseTensor components materialised on the host"

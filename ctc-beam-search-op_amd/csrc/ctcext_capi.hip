@@ -26,6 +26,8 @@ hipError_t launch_decode(const DecodeParams<T>& p, hipStream_t s);
 template <typename T>
 int ring_frames(const DecodeParams<T>& p, int cus, int cap);
 template <typename T>
+bool use_helper_kernel(const DecodeParams<T>& p);
+template <typename T>
 hipError_t launch_row_norm(const T* x, const int32_t* sl, T* norm, int64_t T_, int64_t B, int64_t C,
                            int64_t xstride, hipStream_t s);
 hipError_t launch_traceback(const TraceParams& tp, hipStream_t s);
@@ -117,6 +119,7 @@ struct Dev {
   DevBuf x, sl, norm, prep, rec, foff, item, top_pos, top_kind, logp, seq, len, phase, sctab, gstate;
   int64_t lo = 0, nb = 0;    // this call's shard [lo, lo + nb)
   int ring = 0;              // this call's record-ring frames (ctcx::ring_frames)
+  int rec_bytes = 8;         // this call's record size (8, 16 or 4 bytes)
   int cus = 0;               // compute units of the device
 };
 
@@ -446,7 +449,8 @@ static int enqueue_shard(ctcext_decoder* d, Dev& v, bool root, const ctcext_deco
   tp.rec = p.rec; tp.item = p.item; tp.seq_len = sl; tp.top_pos = p.top_pos; tp.top_kind = p.top_kind;
   tp.Tmax = T_; tp.B = Bs; tp.W = W; tp.P = P; tp.merge = a->merge_repeated ? 1 : 0;
   tp.blank_label = a->blank_label;
-  tp.rec_wide = gs ? 1 : 0;
+  tp.rec_fmt = gs ? ctcx::kRecFmt128 : ctcx::use_helper_kernel<T>(p) ? ctcx::kRecFmt32 : ctcx::kRecFmt64;
+  v.rec_bytes = tp.rec_fmt == ctcx::kRecFmt128 ? 16 : tp.rec_fmt == ctcx::kRecFmt32 ? 4 : 8;
   tp.foff = p.foff;
   tp.seq = (int32_t*)v.seq.p;
   tp.len = (int32_t*)v.len.p;
@@ -550,6 +554,7 @@ static int run_decode(ctcext_decoder* d, const ctcext_decode_args* a, const std:
   d->stats = ctcext_stats{};
   d->stats.tier = use_gstate(a) ? 1 : 0;
   d->stats.ring_frames = root.ring;
+  d->stats.record_bytes = root.rec_bytes;
   if (a->flags & CTCEXT_FLAG_PROFILE) {
     for (int i = 0; i < nd; ++i) {
       Dev& v = d->devs[(size_t)i];

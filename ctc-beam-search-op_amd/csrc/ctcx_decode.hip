@@ -34,6 +34,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "ctcx_kernels.h"
 #include "ctcx_topn.h"
 #include "glibc_math.h"
@@ -3164,8 +3166,26 @@ __host__ __device__ __attribute__((noinline)) int literal_step(Ctx<T> cx, int bu
 // record unreachable now stays unreachable: every later beam descends from a
 // current one.  After the last frame the walk starts from the TopPaths
 // positions alone, and their compacted positions are what top_pos reports.
+// record operations by format (the 8-byte Rec, the two-wave kernel's Rec32)
+template <class RT> struct RecOps;
+template <> struct RecOps<Rec> {
+  __device__ static uint32_t link(Rec r) { return rec_link(r); }
+  __device__ static int label(Rec r) { return rec_label(r); }
+  __device__ static uint32_t bpb(Rec r) { return rec_bp_blank(r); }
+  __device__ static uint32_t bpn(Rec r) { return rec_bp_nblank(r); }
+  __device__ static Rec pack(uint32_t l, int lab, uint32_t b, uint32_t n) { return rec_pack(l, lab, b, n); }
+};
+template <> struct RecOps<Rec32> {
+  __device__ static uint32_t link(Rec32 r) { return r & 255u; }
+  __device__ static int label(Rec32 r) { return (int)((r >> 8) & 63u); }
+  __device__ static uint32_t bpb(Rec32 r) { return rec32_unbp9((r >> 14) & 511u); }
+  __device__ static uint32_t bpn(Rec32 r) { return rec32_unbp9(r >> 23); }
+  __device__ static Rec32 pack(uint32_t l, int lab, uint32_t b, uint32_t n) { return rec32_pack(l, lab, b, n); }
+};
+
+template <class RT = Rec>
 struct Ring {
-  CTCX_LDS Rec* rec;        // [R][W]: frame u in row u & (R - 1)
+  CTCX_LDS RT* rec;         // [R][W]: frame u in row u & (R - 1)
   CTCX_LDS int* rn;         // [R]: entries of each ring frame
   CTCX_LDS int16_t* tbl;    // [2][W]: compacted positions, by frame parity
   CTCX_LDS int16_t* sv;     // [2][W]: the newest written frame's, by flush parity
@@ -3173,12 +3193,13 @@ struct Ring {
   int R, W;
 };
 
-__device__ __forceinline__ Ring ring_carve(CTCX_LDS char* p, int R, int W) {
+template <class RT = Rec>
+__device__ __forceinline__ Ring<RT> ring_carve(CTCX_LDS char* p, int R, int W) {
   auto a16 = [](size_t v) { return (v + 15) & ~(size_t)15; };
-  Ring g;
+  Ring<RT> g;
   g.R = R;
   g.W = W;
-  g.rec = (CTCX_LDS Rec*)p; p += (size_t)R * W * 8;
+  g.rec = (CTCX_LDS RT*)p; p += a16((size_t)R * W * sizeof(RT));
   g.rn = (CTCX_LDS int*)p; p += a16(4 * (size_t)R);
   g.tbl = (CTCX_LDS int16_t*)p; p += a16(4 * (size_t)W);
   g.sv = (CTCX_LDS int16_t*)p; p += a16(4 * (size_t)W);
@@ -3209,11 +3230,13 @@ __device__ __forceinline__ int ring_rank(const bool (&a)[KM], int (&rk)[KM]) {
 // positions and records stay in registers; a frame's reachable records stamp
 // their targets one frame down (a value unique to this flush and step, so the
 // stamps need no clearing), and the compacted positions go to LDS for the
-// renumbering gathers.
-template <int KM>
-__device__ void ring_flush(const Ring& g, Rec* out, int32_t* foff, int t_new, int u_lo, int u_hi,
+// renumbering gathers.  ONE: a single wave runs it (the two-wave kernel's
+// helper), so its barriers are wave-local.
+template <int KM, class RT = Rec, bool ONE = false>
+__device__ void ring_flush(const Ring<RT>& g, RT* out, int32_t* foff, int t_new, int u_lo, int u_hi,
                            const CTCX_LDS int* tops, int ntops, int fp, int& cursor) {
-  const int lane = threadIdx.x, M = g.R - 1, W = g.W;
+  using RO = RecOps<RT>;
+  const int lane = threadIdx.x & 63, M = g.R - 1, W = g.W;
   const int sbase = fp * 4096;   // stamps of this flush: sbase + (t_new - frame) + 1; R <= 256
   bool al[KM];
   int rk[KM];
@@ -3221,7 +3244,7 @@ __device__ void ring_flush(const Ring& g, Rec* out, int32_t* foff, int t_new, in
     const int n = g.rn[t_new & M];
     if (tops != nullptr) {
       for (int q = lane; q < ntops; q += 64) g.st[(t_new & 1) * W + tops[q]] = sbase;
-      __syncthreads();
+      wsync<ONE>();
     }
 #pragma unroll
     for (int j = 0; j < KM; ++j) {
@@ -3231,10 +3254,10 @@ __device__ void ring_flush(const Ring& g, Rec* out, int32_t* foff, int t_new, in
   }
   int cnt = ring_rank<KM>(al, rk);
   for (int u = t_new; u >= u_lo; --u) {
-    const CTCX_LDS Rec* ru = g.rec + (size_t)(u & M) * W;
-    Rec r[KM];
+    const CTCX_LDS RT* ru = g.rec + (size_t)(u & M) * W;
+    RT r[KM];
 #pragma unroll
-    for (int j = 0; j < KM; ++j) r[j] = al[j] ? ru[lane + 64 * j] : 0ull;
+    for (int j = 0; j < KM; ++j) r[j] = al[j] ? ru[lane + 64 * j] : (RT)0;
     bool al1[KM];
     int rk1[KM], cnt1 = 0;
     if (u > u_lo) {
@@ -3244,13 +3267,13 @@ __device__ void ring_flush(const Ring& g, Rec* out, int32_t* foff, int t_new, in
 #pragma unroll
       for (int j = 0; j < KM; ++j) {
         if (al[j]) {
-          const uint32_t qb = rec_bp_blank(r[j]), qn = rec_bp_nblank(r[j]);
-          s1[rec_link(r[j]) >> 1] = sv1;
+          const uint32_t qb = RO::bpb(r[j]), qn = RO::bpn(r[j]);
+          s1[RO::link(r[j]) >> 1] = sv1;
           if (qb < kBpRestart) s1[qb >> 1] = sv1;
           if (qn < kBpRestart) s1[qn >> 1] = sv1;
         }
       }
-      __syncthreads();
+      wsync<ONE>();
       const int n1 = g.rn[(u - 1) & M];
 #pragma unroll
       for (int j = 0; j < KM; ++j) {
@@ -3263,7 +3286,7 @@ __device__ void ring_flush(const Ring& g, Rec* out, int32_t* foff, int t_new, in
 #pragma unroll
         for (int j = 0; j < KM; ++j)
           if (al1[j]) t1[lane + 64 * j] = (int16_t)rk1[j];
-        __syncthreads();
+        wsync<ONE>();
       }
     }
     if (u <= u_hi) {
@@ -3278,13 +3301,13 @@ __device__ void ring_flush(const Ring& g, Rec* out, int32_t* foff, int t_new, in
 #pragma unroll
       for (int j = 0; j < KM; ++j) {
         if (al[j]) {
-          uint32_t lk = rec_link(r[j]), qb = rec_bp_blank(r[j]), qn = rec_bp_nblank(r[j]);
+          uint32_t lk = RO::link(r[j]), qb = RO::bpb(r[j]), qn = RO::bpn(r[j]);
           if (u > 0) {
             lk = ((uint32_t)tp[lk >> 1] << 1) | (lk & 1u);
             if (qb < kBpRestart) qb = ((uint32_t)tp[qb >> 1] << 1) | (qb & 1u);
             if (qn < kBpRestart) qn = ((uint32_t)tp[qn >> 1] << 1) | (qn & 1u);
           }
-          out[cursor + rk[j]] = rec_pack(lk, rec_label(r[j]), qb, qn);
+          out[cursor + rk[j]] = RO::pack(lk, RO::label(r[j]), qb, qn);
         }
       }
       if (lane == 0) foff[u] = cursor;
@@ -3294,7 +3317,7 @@ __device__ void ring_flush(const Ring& g, Rec* out, int32_t* foff, int t_new, in
     for (int j = 0; j < KM; ++j) { al[j] = al1[j]; rk[j] = rk1[j]; }
     cnt = cnt1;
   }
-  __syncthreads();
+  wsync<ONE>();
 }
 
 // HW: two waves per item (wave 1 the helper, see help_score_chunks); every
@@ -3327,21 +3350,26 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
   CTCX_LDS int* const misc = cx.misc;
   // the record ring (host: ring_frames) after the decode layout; R = 0 writes
   // every record to rec[b][t][k]
+  // HW kernels: 4-byte records, the score table after the decode layout,
+  // then the ring, whose flushes the helper wave runs
   const int R = prm.ring;
-  Ring rg{};
-#ifndef CTCX_GSTATE
-  if (R > 0)
-    rg = ring_carve((CTCX_LDS char*)lds + ((decode_lds_bytes(WC > 0 ? WC : W, C, (int)sizeof(T), SC::kStateful) +
-                                            15) & ~(size_t)15), R, W);
-#endif
+  using RT = typename std::conditional<HW, Rec32, Rec>::type;
+  Ring<RT> rg{};
   Tab tb{};
 #ifndef CTCX_GSTATE
-  if constexpr (HW)   // the score table after the decode layout (no record ring in HW kernels)
-    tb = tab_carve((CTCX_LDS char*)lds + ((decode_lds_bytes(WC, C, (int)sizeof(T), false) + 15) & ~(size_t)15));
+  {
+    size_t off = (decode_lds_bytes(WC > 0 ? WC : W, C, (int)sizeof(T), SC::kStateful) + 15) & ~(size_t)15;
+    if constexpr (HW) {
+      tb = tab_carve((CTCX_LDS char*)lds + off);
+      off += tab_lds_bytes();
+    }
+    if (R > 0) rg = ring_carve<RT>((CTCX_LDS char*)lds + off, R, W);
+  }
 #endif
   if (R > 0)
     for (int k = lane; k < 2 * W; k += 64) rg.st[k] = -1;   // no stamp yet
-  Rec* const rstream = prm.rec + b * prm.Tmax * W;   // item b's record stream (ring)
+  RT* const rstream = (RT*)prm.rec + b * prm.Tmax * W;   // item b's record stream (ring)
+  int pf_t = -1, pf_lo = 0, pf_hi = 0, pf_fp = 0;      // HW: a ring flush pending for the helper
   int32_t* const foff = prm.foff ? prm.foff + b * prm.Tmax : nullptr;
   int flushed = 0, nflush = 0, nrec = 0;   // first frame not yet in HBM, flushes, ring stream cursor
   int64_t nrec_all = 0;                    // records written without the ring (T * W can pass 2^31)
@@ -3431,6 +3459,9 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
         cx.misc[5] = n;
         cx.misc[6] = nl_fast;
       }
+      if (tid >= 64 && pf_t >= 0)   // the helper: the flush the previous commit left pending
+        ring_flush<2, RT, true>(rg, rstream, foff, pf_t, pf_lo, pf_hi, nullptr, 0, pf_fp, nrec);
+      pf_t = -1;
       __syncthreads();
       why = uni(cx.misc[4]);
       n = uni(cx.misc[5]);
@@ -3548,8 +3579,9 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
 #ifdef CTCX_GSTATE
       ((Rec16*)prm.rec)[((int64_t)b * prm.Tmax + t) * W + k] = Rec16{kd, cx.elab[e], bpb, bpn};
 #else
-      if (R > 0) rg.rec[(t & (R - 1)) * W + k] = rec_pack(kd, cx.elab[e], bpb, bpn);
-      else prm.rec[((int64_t)b * prm.Tmax + t) * W + k] = rec_pack(kd, cx.elab[e], bpb, bpn);
+      const RT rc = RecOps<RT>::pack(kd, cx.elab[e], bpb, bpn);
+      if (R > 0) rg.rec[(t & (R - 1)) * W + k] = rc;
+      else rstream[(int64_t)t * W + k] = rc;
 #endif
     };
     if constexpr (STAGED) {
@@ -3604,7 +3636,13 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
     }
     if (R == 0) nrec_all += n;
     else if (t - flushed + 1 == R) {   // the ring is full: write its older half
-      ring_flush<KM>(rg, rstream, foff, t, flushed, flushed + R / 2 - 1, nullptr, 0, nflush, nrec);
+      if constexpr (HW) {
+        // the helper flushes during the next frame's grow (its rows stay intact
+        // until that frame's commit, behind the barrier after exact_step)
+        pf_t = t; pf_lo = flushed; pf_hi = flushed + R / 2 - 1; pf_fp = nflush;
+      } else {
+        ring_flush<KM>(rg, rstream, foff, t, flushed, flushed + R / 2 - 1, nullptr, 0, nflush, nrec);
+      }
       flushed += R / 2;
       ++nflush;
     }
@@ -3618,8 +3656,20 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
   if (sl == 0 && tid == 0) cx.tops[0] = 0;
   __syncthreads();
   const int np = (prm.P < n_leaves) ? prm.P : n_leaves;
-  // the rest of the ring, walked from the TopPaths positions
-  if (R > 0 && sl > 0) ring_flush<(WC > 0 ? WC : 512) / 64>(rg, rstream, foff, sl - 1, flushed, sl - 1, cx.tops, np, nflush, nrec);
+  // the rest of the ring, walked from the TopPaths positions (HW: by the
+  // helper, after the flush the last commit may have left pending; its
+  // stream cursor is then the item's record count)
+  if constexpr (HW) {
+    if (R > 0 && sl > 0 && tid >= 64) {
+      if (pf_t >= 0) ring_flush<2, RT, true>(rg, rstream, foff, pf_t, pf_lo, pf_hi, nullptr, 0, pf_fp, nrec);
+      ring_flush<2, RT, true>(rg, rstream, foff, sl - 1, flushed, sl - 1, cx.tops, np, nflush, nrec);
+      if (tid == 64) misc[13] = nrec;
+    }
+    __syncthreads();
+    if (R > 0 && sl > 0) nrec = misc[13];
+  } else {
+    if (R > 0 && sl > 0) ring_flush<(WC > 0 ? WC : 512) / 64>(rg, rstream, foff, sl - 1, flushed, sl - 1, cx.tops, np, nflush, nrec);
+  }
   for (int q = tid; q < prm.P; q += NT) {
     int pos = -1, kind = -1, opos = -1;
     T lp = T(0);
@@ -4171,9 +4221,13 @@ __global__ __launch_bounds__(256) void ctcx_traceback(TraceParams tp) {
     // record (t, k) unpacked: link, label, the two alignment back-pointers
     auto rd = [&](int t, uint32_t& link, int& lab, uint32_t& bpb, uint32_t& bpn) {
       const int64_t at = tp.foff ? b * tp.Tmax * tp.W + tp.foff[b * tp.Tmax + t] + k : (b * tp.Tmax + t) * tp.W + k;
-      if (tp.rec_wide) {
+      if (tp.rec_fmt == kRecFmt128) {
         const Rec16 r = ((const Rec16*)tp.rec)[at];
         link = r.link; lab = r.label; bpb = r.bpb; bpn = r.bpn;
+      } else if (tp.rec_fmt == kRecFmt32) {
+        const Rec32 r = ((const Rec32*)tp.rec)[at];
+        link = r & 255u; lab = (int)((r >> 8) & 63u); bpb = rec32_unbp9((r >> 14) & 511u);
+        bpn = rec32_unbp9(r >> 23);
       } else {
         const Rec r = tp.rec[at];
         link = rec_link(r); lab = rec_label(r); bpb = rec_bp_blank(r); bpn = rec_bp_nblank(r);
@@ -4269,12 +4323,10 @@ namespace ctcx {
 
 template <typename T, int RN, int WC, bool BIG, class SC, bool HW = false>
 hipError_t launch_decode_c(const DecodeParams<T>& p, hipStream_t s) {
+  // the decode layout, then (HW) the score table, then the record ring
   size_t lds = decode_lds_bytes(WC > 0 ? WC : p.W, p.C, (int)sizeof(T), SC::kStateful);
-  if (p.ring > 0) lds = ((lds + 15) & ~(size_t)15) + ring_lds_bytes(p.ring, p.W);
-  if (HW) {
-    if (p.ring > 0) return hipErrorInvalidValue;   // (the dispatcher never asks: no ring in HW kernels)
-    lds = ((lds + 15) & ~(size_t)15) + tab_lds_bytes();
-  }
+  if (HW) lds = ((lds + 15) & ~(size_t)15) + tab_lds_bytes();
+  if (p.ring > 0) lds = ((lds + 15) & ~(size_t)15) + ring_lds_bytes(p.ring, p.W, HW ? 4 : 8);
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)ctcx_beam_decode<T, RN, WC, BIG, SC, HW>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -4379,6 +4431,32 @@ static hipError_t launch_decode_r(const DecodeParams<T>& p, hipStream_t s) {
   return p.C > 64 ? launch_decode_c<T, RN, WC, true, SC>(p, s) : launch_decode_c<T, RN, WC, false, SC>(p, s);
 }
 
+// float, beams <= 128, C <= 64, the base scorer, no record ring: the two-wave
+// kernel, which writes 4-byte records (CTCEXT_HELPER=0, diagnostics: the
+// one-wave kernel instead)
+template <typename T>
+bool helper_shape(const DecodeParams<T>& p) {
+  if (sizeof(T) != 4 || p.scorer_tab != nullptr || p.W > kRec32MaxBeam || p.C > kRec32MaxClasses) return false;
+  const char* hv = getenv("CTCEXT_HELPER");
+  return !(hv && hv[0] == '0');
+}
+// LDS bytes before the record ring: the decode layout and, for the two-wave
+// kernel, its score table
+template <typename T>
+size_t pre_ring_lds_bytes(const DecodeParams<T>& p, bool hw, int wc) {
+  size_t b = (decode_lds_bytes(wc, p.C, (int)sizeof(T), p.scorer_tab != nullptr) + 15) & ~(size_t)15;
+  return hw ? b + tab_lds_bytes() : b;
+}
+template <typename T>
+bool use_helper_kernel(const DecodeParams<T>& p) {
+  if (!helper_shape(p)) return false;
+  size_t b = pre_ring_lds_bytes(p, true, 128);
+  if (p.ring > 0) b = ((b + 15) & ~(size_t)15) + ring_lds_bytes(p.ring, p.W, 4);
+  return b <= kLdsBytes;
+}
+template bool use_helper_kernel<float>(const DecodeParams<float>&);
+template bool use_helper_kernel<double>(const DecodeParams<double>&);
+
 template <typename T>
 hipError_t launch_decode(const DecodeParams<T>& p, hipStream_t s) {
   if (p.B == 0) return hipSuccess;
@@ -4392,14 +4470,8 @@ hipError_t launch_decode(const DecodeParams<T>& p, hipStream_t s) {
     return launch_decode_r<T, 4, 0, SC>(p, s);
   }
   auto fits = [&](int wc) { return decode_lds_bytes(wc, p.C, (int)sizeof(T), false) <= kLdsBytes; };
-  if constexpr (sizeof(T) == 4) {
-    // float, beams <= 128, C <= 64, no record ring: the two-wave kernel
-    // (CTCEXT_HELPER=0, diagnostics: the one-wave kernel instead)
-    const char* hv = getenv("CTCEXT_HELPER");
-    if (p.W <= 128 && p.C <= 64 && p.ring == 0 && !(hv && hv[0] == '0') &&
-        ((decode_lds_bytes(128, p.C, 4, false) + 15) & ~(size_t)15) + tab_lds_bytes() <= kLdsBytes)
-      return launch_decode_c<float, 1, 128, false, BaseBeamScorer<float>, true>(p, s);
-  }
+  if constexpr (sizeof(T) == 4)
+    if (use_helper_kernel(p)) return launch_decode_c<float, 1, 128, false, BaseBeamScorer<float>, true>(p, s);
   if (p.W <= 128) return fits(128) ? launch_decode_r<T, 1, 128>(p, s) : launch_decode_r<T, 1, 0>(p, s);
   if (p.W <= 256) return fits(256) ? launch_decode_r<T, 2, 256>(p, s) : launch_decode_r<T, 2, 0>(p, s);
   return launch_decode_r<T, 4, 0>(p, s);
@@ -4419,7 +4491,10 @@ int ring_frames(const DecodeParams<T>& p, int cus, int cap) {
   auto fits = [&](int wc) { return decode_lds_bytes(wc, p.C, (int)sizeof(T), scored) <= kLdsBytes; };
   const int wcap = (p.W <= 128 && fits(128)) ? 128 : (p.W > 128 && p.W <= 256 && fits(256)) ? 256 : p.W;
   if ((int64_t)p.Tmax * p.W > 0x7fffffffLL) return 0;
-  const size_t base = (decode_lds_bytes(wcap, p.C, (int)sizeof(T), scored) + 15) & ~(size_t)15;
+  // the two-wave kernel (when its layout and a ring fit): table + 4-byte records
+  const bool hw = helper_shape(p) && pre_ring_lds_bytes(p, true, 128) + ring_lds_bytes(8, p.W, 4) <= kLdsBytes;
+  const int rb = hw ? 4 : 8;
+  const size_t base = pre_ring_lds_bytes(p, hw, hw ? 128 : wcap);
   const size_t budget = (base > 80 * 1024 || p.B <= cus) ? kLdsBytes : 80 * 1024;
   // the kernel addresses ring rows by t & (R - 1): R must be a power of two
   if (cap < 8) return 0;
@@ -4428,7 +4503,7 @@ int ring_frames(const DecodeParams<T>& p, int cus, int cap) {
     // ring_flush's stamps are fp * 4096 + (step + 1), fp the flush count
     // (<= Tmax / (R / 2) + 1): they must stay below INT32_MAX
     if (((int64_t)p.Tmax / (r / 2) + 2) * 4096 > 0x7fffffffLL) continue;
-    if (base + ring_lds_bytes(r, p.W) <= budget) return r;
+    if (base + ring_lds_bytes(r, p.W, rb) <= budget) return r;
   }
   return 0;
 }

@@ -49,6 +49,25 @@ __host__ __device__ inline uint32_t rec_bp_nblank(Rec r) { return rec_unbp12((r 
 constexpr int kMaxRecClasses = 65535;
 constexpr int kMaxRecBeam = 512;
 
+// The 4-byte record of the two-wave kernel (beam_width <= 128, num_classes <=
+// 64): the same fields, narrower:
+//   bits  0..7   link = (src branch << 1) | is_new_child   (src < 128)
+//   bits  8..13  label (0..63; the root's -1 is stored as 63 and never read:
+//                the root is never a new child and has no label-ending candidate)
+//   bits 14..22  best blank-ending alignment back-pointer (pos << 1 | kind),
+//   bits 23..31  best label-ending one; 256 = restart or none (the traceback
+//                stops at either and never follows a candidate that is absent)
+typedef uint32_t Rec32;
+__host__ __device__ inline uint32_t rec32_bp9(uint32_t q) { return q >= kBpRestart ? 256u : q; }
+__host__ __device__ inline Rec32 rec32_pack(uint32_t link, int label, uint32_t bp_blank, uint32_t bp_nblank) {
+  return link | ((uint32_t)(label & 63) << 8) | (rec32_bp9(bp_blank) << 14) | (rec32_bp9(bp_nblank) << 23);
+}
+__host__ __device__ inline uint32_t rec32_unbp9(uint32_t v) { return v >= 256u ? kBpRestart : v; }
+constexpr int kRec32MaxBeam = 128;
+constexpr int kRec32MaxClasses = 64;
+// record formats (TraceParams::rec_fmt)
+constexpr int kRecFmt64 = 0, kRecFmt128 = 1, kRecFmt32 = 2;
+
 // The wide record of the global-state tier (any beam width and num_classes):
 // the same four fields at full width, 16 bytes.
 struct Rec16 {
@@ -135,7 +154,7 @@ struct TraceParams {
   const int32_t* top_kind;
   int64_t Tmax, B;
   int32_t W, P, merge, blank_label;
-  int32_t rec_wide;   // records are Rec16 (global-state tier), else Rec
+  int32_t rec_fmt;    // kRecFmt64 (Rec), kRecFmt128 (Rec16, global-state tier), kRecFmt32 (Rec32, two-wave kernel)
   const int32_t* foff;   // record ring: frame t of item b at rec + b * Tmax * W + foff[b][t] (null: [b][t][W])
   int32_t* seq;    // [B][P][2][Tmax]  walk output, reversed
   int32_t* len;    // [P][2][len_stride], this batch's items at [.][.][0, B)
@@ -179,9 +198,9 @@ __host__ __device__ inline bool decode_inplace(int64_t C) { return C > 64; }
 // aligned): the records [R][W], entries per frame [R], compacted positions by
 // frame parity [2][W] and of the newest written frame by flush parity [2][W]
 // (int16), reachability stamps by frame parity [2][W] (int32).
-__host__ __device__ inline size_t ring_lds_bytes(int R, int W) {
+__host__ __device__ inline size_t ring_lds_bytes(int R, int W, int rec_bytes = 8) {
   auto a16 = [](size_t v) { return (v + 15) & ~(size_t)15; };
-  return (size_t)R * (size_t)W * 8 + a16(4 * (size_t)R) + 2 * a16(4 * (size_t)W) + a16(8 * (size_t)W);
+  return a16((size_t)R * (size_t)W * rec_bytes) + a16(4 * (size_t)R) + 2 * a16(4 * (size_t)W) + a16(8 * (size_t)W);
 }
 
 // Bytes of the decode kernel's LDS layout for a beam capacity W (carve() in

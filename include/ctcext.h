@@ -125,6 +125,10 @@ typedef struct {
   int32_t ring_frames;             /* last decode: frames of the LDS record ring (0: every
                                       record of every frame written to HBM) */
   int64_t records_written;         /* last decode: beam records written to HBM (all devices) */
+  int32_t record_bytes;            /* last decode: bytes per record (8; 16 on the global-state
+                                      tier; 4 in the two-wave kernel, beam_width <= 128 and
+                                      num_classes <= 64) */
+  int32_t pad_;
 } ctcext_stats;
 
 /* Handle lifetime.  A handle owns a HIP stream and a grow-only device
