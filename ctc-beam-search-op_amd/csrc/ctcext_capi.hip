@@ -26,7 +26,7 @@ hipError_t launch_decode(const DecodeParams<T>& p, hipStream_t s);
 template <typename T>
 int ring_frames(const DecodeParams<T>& p, int cus, int cap);
 template <typename T>
-bool use_helper_kernel(const DecodeParams<T>& p);
+int use_helper_kernel(const DecodeParams<T>& p);
 template <typename T>
 hipError_t launch_row_norm(const T* x, const int32_t* sl, T* norm, int64_t T_, int64_t B, int64_t C,
                            int64_t xstride, hipStream_t s);
@@ -449,7 +449,7 @@ static int enqueue_shard(ctcext_decoder* d, Dev& v, bool root, const ctcext_deco
   tp.rec = p.rec; tp.item = p.item; tp.seq_len = sl; tp.top_pos = p.top_pos; tp.top_kind = p.top_kind;
   tp.Tmax = T_; tp.B = Bs; tp.W = W; tp.P = P; tp.merge = a->merge_repeated ? 1 : 0;
   tp.blank_label = a->blank_label;
-  tp.rec_fmt = gs ? ctcx::kRecFmt128 : ctcx::use_helper_kernel<T>(p) ? ctcx::kRecFmt32 : ctcx::kRecFmt64;
+  tp.rec_fmt = gs ? ctcx::kRecFmt128 : ctcx::use_helper_kernel<T>(p) == 1 ? ctcx::kRecFmt32 : ctcx::kRecFmt64;
   v.rec_bytes = tp.rec_fmt == ctcx::kRecFmt128 ? 16 : tp.rec_fmt == ctcx::kRecFmt32 ? 4 : 8;
   tp.foff = p.foff;
   tp.seq = (int32_t*)v.seq.p;

@@ -1713,9 +1713,320 @@ __device__ __forceinline__ void help_score_chunks(const Ctx<T>& cx, Tab tb, int 
   }
 }
 
+// large C, the beam full: one compacted chunk.  The offers of the span from
+// (i0, li0) on that can have an effect are gathered, in offer order, into cq
+// (up to 64): a new child whose score can beat the bottom ((x_l - norm) + ot
+// > bottom bounds the score; bottom only rises, so an offer failing it now
+// fails at its turn too) and every re-offer of a branch child (evicted now,
+// or by an event of this chunk before it).  The rest of the span is rejected
+// by the reference without effect.  Branch turns are checked here at the
+// given bottom (closed now: closed at its turn, the grow ends after this
+// chunk: gstop) and again in the chunk at the bottom its turn sees (sl, bat).
+// Any bottom at or below the true one gives a correct chunk (a superset of
+// the offers that can have an effect): the two-wave kernels' helper gathers
+// with the last bottom wave 0 published.  cbr: the branch whose children the
+// child bitmap holds (row_cbm), kept across chunks.
+template <typename T>
+__device__ __forceinline__ void gather_chunk(const Ctx<T>& cx, int buf, int nb, T norm, T pmax, T bottom, int tsn,
+                                             T txo, int& i0, int& li0, int& cbr, bool& gstop,
+                                             CTCX_LDS uint32_t* cq, int& cqn, uint64_t* pc) {
+  const int lane = threadIdx.x & 63;
+  const T NI = ninf<T>();
+  const int Cm1 = cx.C - 1;
+  const int blank = cx.blank;
+  CTCX_LDS T* bmax = row_bmax(cx);
+    CTCX_LDS uint64_t* cbm = row_cbm(cx);
+    CTCX_LDS uint64_t* cwin = cbm + (Cm1 + 63) / 64;
+    cqn = 0;
+    // the branch scan (lane j: branch sb + j) and a branch's window scan
+    // (lane w: window wa0 + w) hold for the whole gather: no event moves the
+    // bottom before the chunk runs
+    int sb = -1, wa0 = -1;
+    uint64_t hitM = 0, brkM = 0, chM = 0, wkM = 0;
+    T otb = NI, ot0 = NI;
+    bool enter = true;   // at the gather's start or a branch's first offer
+    const uint64_t tg0 = pc ? __builtin_amdgcn_s_memtime() : 0;
+    const T tsx = lane < tsn ? (T)row_topx(cx)[lane] : NI;                          // S in label-index order:
+    const int tsl = lane < tsn ? ((CTCX_LDS int*)(row_topx(cx) + kTopK))[lane] : Cm1;   // lane j its j-th
+    while (cqn < 64) {
+      const uint64_t te0 = pc ? __builtin_amdgcn_s_memtime() : 0;
+      if (enter) {
+        // the next branch with a turn closed (stop), or with something to
+        // gather (pmax + ot > bottom, or children)
+        int res = 0;   // 0: at a branch to gather from, 1: a turn is closed, 2: past the last branch
+        for (;;) {
+          if (sb < 0 || i0 >= sb + 64) {
+            sb = i0;
+            const int ib = i0 + lane;
+            bool brk = false, skp = true, ch = false;
+            otb = NI;
+            if (ib < nb) {
+              otb = sel(cx.ot, buf)[ib];
+              ch = cx.head[ib] >= 0;
+              brk = (lane > 0 || li0 == 0) && !(otb > bottom);
+              skp = !(pmax + otb > bottom) && !ch;
+            }
+            hitM = __ballot(brk || !skp);
+            brkM = __ballot(brk);
+            chM = __ballot(ch);
+          }
+          const uint64_t m = hitM & ~lowmask(i0 - sb);
+          if (m == 0) {
+            i0 = sb + 64;
+            li0 = 0;
+            if (i0 >= nb) { res = 2; break; }
+            continue;
+          }
+          const int k = (int)__builtin_ctzll(m);
+          if (sb + k > i0) li0 = 0;
+          i0 = sb + k;
+          if ((brkM >> k) & 1ull) res = 1;
+          ot0 = bcast(otb, k);
+          const int nbr = ((chM >> k) & 1ull) ? i0 : -1;
+          if (nbr != cbr) {
+            cq_children(cx, buf, nb, cbr, nbr);
+            cbr = nbr;
+          }
+          break;
+        }
+        if (pc) pc[20] += __builtin_amdgcn_s_memtime() - te0;
+        if (res == 1) gstop = true;
+        if (res != 0) break;
+        if (pc) pc[21] += 1;
+        enter = false;
+        wa0 = -1;
+      }
+      if (tsn > 0 && !(((txo - norm) + ot0) > bottom)) {
+        if (pc) pc[22] += 1;
+        if (li0 == 0 && cbr != i0) {
+          // a run of branches i0, i0 + 1, ... (lane L: branch i0 + L) each
+          // with every candidate in S, no branch children and an open turn
+          // (branch i0's was checked by the branch scan): each takes one
+          // ballot of its S offers that beat the bound, in branch order,
+          // while they fit the chunk -- the same decisions and entries as
+          // the per-branch path below, without its branch selection
+          const int ib = i0 + lane;
+          const bool vb = ib < nb;
+          const T otL = vb ? sel(cx.ot, buf)[ib] : NI;
+          const bool okL = vb && (otL > bottom) && cx.head[ib] < 0 && !(((txo - norm) + otL) > bottom);
+          const uint64_t badM = ~__ballot(okL || lane == 0);
+          const int R = badM ? (int)__builtin_ctzll(badM) : 64;   // run length (>= 1)
+          const T sxv = tsx - norm;                                // S lane j: x_j - norm
+          int L = 0;
+          for (; L < R; ++L) {
+            const T ob = bcast(otL, L);
+            const bool h = lane < tsn && ((sxv + ob) > bottom);
+            const uint64_t hM = __ballot(h);
+            const int nh = __builtin_popcountll(hM);
+            if (nh > 64 - cqn) break;
+            if (h) {
+              const int r = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(hM >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((unsigned)hM, 0u));
+              cq[cqn + r] = ((uint32_t)(i0 + L) << 16) | (uint32_t)tsl;
+            }
+            cqn += nh;
+          }
+          if (L > 0) {
+            i0 += L;
+            li0 = 0;
+            enter = true;
+            if (i0 >= nb) break;
+            continue;
+          }
+        }
+        // every candidate of branch i0 is in S: its offers from li0 on that
+        // beat the bound, merged in label order with its children (from the
+        // bitmap, ascending); a branch that does not fit the chunk's room
+        // starts the next chunk (or, first in the chunk, goes by windows)
+        const bool hot = tsl >= li0 && (((tsx - norm) + ot0) > bottom);
+        const uint64_t hotM = __ballot(hot);
+        const int nh = __builtin_popcountll(hotM);
+        int padd = 0, nch = 0;
+        if (cbr == i0) {
+          for (int q = 0; q * 64 < (Cm1 + 63) / 64; ++q) {
+            uint64_t wq = uni64(cwin[q]);
+            while (wq) {
+              const int a = q * 64 + (int)__builtin_ctzll(wq);
+              wq &= wq - 1ull;
+              uint64_t bits = uni64(cbm[a]);
+              if (a * 64 < li0) bits &= ~lowmask(li0 - a * 64);
+              while (bits) {
+                const int xc = a * 64 + (int)__builtin_ctzll(bits);
+                bits &= bits - 1ull;
+                if (__ballot(hot && tsl == xc)) continue;   // also a hot offer of S
+                const int pos = cqn + __builtin_popcountll(hotM & __ballot(tsl < xc)) + nch;
+                if (lane == 0 && pos < 64) cq[pos] = ((uint32_t)i0 << 16) | (uint32_t)xc;
+                padd += (tsl > xc) ? 1 : 0;
+                ++nch;
+              }
+            }
+          }
+        }
+        if (pc) pc[23] += __builtin_amdgcn_s_memtime() - te0;
+        if (nh + nch <= 64 - cqn) {
+          if (hot) {
+            const int r = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(hotM >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((unsigned)hotM, 0u));
+            cq[cqn + r + padd] = ((uint32_t)i0 << 16) | (uint32_t)tsl;
+          }
+          cqn += nh + nch;
+          ++i0;
+          li0 = 0;
+          enter = true;
+          if (i0 >= nb) break;
+          continue;
+        }
+        if (cqn > 0) break;
+      }
+      // branch i0's aligned 64-label windows from li0 on (lane w: window
+      // wa0 + w): one whose labels' block maxima bound every score
+      // (xb - norm) + ot0 <= bottom and that holds no child is passed over
+      const uint64_t tw0 = pc ? __builtin_amdgcn_s_memtime() : 0;
+      if (pc) pc[17] += 1;
+      if (wa0 < 0 || (li0 >> 6) >= wa0 + 64) {
+        wa0 = li0 >> 6;
+        const int lw = (wa0 + lane) * 64;
+        bool keep = false;
+        if (lw < Cm1) {
+          const int le = (lw + 64 < Cm1 ? lw + 64 : Cm1) - 1;
+          const int la = lw + (lw >= blank ? 1 : 0);
+          const int lb = le + (le >= blank ? 1 : 0);
+          const T ba = bmax[la >> 6], bb = bmax[lb >> 6];
+          const T xb = ba > bb ? ba : bb;
+          const int a = wa0 + lane;
+          keep = (((xb - norm) + ot0) > bottom) || (((cwin[a >> 6] >> (a & 63)) & 1ull) != 0);
+        }
+        wkM = __ballot(keep);
+      }
+      uint64_t m = wkM & ~lowmask((li0 >> 6) - wa0);
+      int nli0;
+      if (m == 0) {
+        nli0 = (wa0 + 64) * 64;
+      } else {
+        // up to kGatherWin kept windows per batch of row reads: the exact
+        // per-label bound, and the children
+        int aw[kGatherWin];
+        T xv[kGatherWin];
+        uint64_t cw[kGatherWin];
+#pragma unroll
+        for (int j = 0; j < kGatherWin; ++j) {
+          aw[j] = -1;
+          if (m) {
+            aw[j] = wa0 + (int)__builtin_ctzll(m);
+            m &= m - 1ull;
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < kGatherWin; ++j) {
+          xv[j] = NI;
+          cw[j] = 0ull;
+          if (aw[j] >= 0) {
+            const int x = aw[j] * 64 + lane;
+            const int xc = x < Cm1 ? x : Cm1 - 1;
+            xv[j] = cx.row[xc + (xc >= blank ? 1 : 0)];
+            cw[j] = cbm[aw[j]];
+          }
+        }
+        nli0 = -1;
+        int endw = 0;
+#pragma unroll
+        for (int j = 0; j < kGatherWin; ++j) {
+          if (aw[j] >= 0 && nli0 < 0 && cqn < 64) {
+            const int wb = aw[j] * 64;
+            const int x = wb + lane;
+            const bool hot = x >= li0 && x < Cm1 &&
+                             ((((xv[j] - norm) + ot0) > bottom) || (((cw[j] >> lane) & 1ull) != 0));
+            uint64_t hotM = __ballot(hot);
+            const int rank =
+                (int)__builtin_amdgcn_mbcnt_hi((unsigned)(hotM >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)hotM, 0u));
+            if (__builtin_popcountll(hotM) > 64 - cqn) {   // the chunk fills here
+              hotM = __ballot(hot && rank < 64 - cqn);
+              nli0 = wb + 64 - __builtin_clzll(hotM);
+            }
+            if ((hotM >> lane) & 1ull) cq[cqn + rank] = ((uint32_t)i0 << 16) | (uint32_t)x;
+            cqn += __builtin_popcountll(hotM);
+            endw = wb + 64;
+          }
+        }
+        if (nli0 < 0) nli0 = endw;
+      }
+      li0 = nli0;
+      if (pc) pc[18] += __builtin_amdgcn_s_memtime() - tw0;
+      if (li0 >= Cm1) {
+        ++i0;
+        li0 = 0;
+        enter = true;
+        if (i0 >= nb) break;
+      }
+    }
+  if (pc) pc[16] += __builtin_amdgcn_s_memtime() - tg0;
+}
+
+// The gather queue of the two-wave large-C kernels: wave 1 gathers the
+// frame's compacted chunks (gather_chunk, with the last bottom wave 0
+// published: a superset of the offers that can have an effect, see there)
+// into a ring of kQSlots chunks; wave 0 takes them in order and runs their
+// events.  A chunk with cqn = 0 ends the frame's grow (gstop: a closed turn).
+// Hand-over as for the score table (kCtlReady / kCtlCons / kCtlDone), plus
+// wave 0's bottom after every chunk (kCtlBot, float bits).
+constexpr int kQSlots = 4;
+constexpr int kCtlBot = 12;
+struct GQ {
+  CTCX_LDS uint32_t* e;     // [slot][64]: (branch << 16) | label index
+  CTCX_LDS int* h;          // [slot][4]: cqn, span start (branch, label index), gstop
+};
+__host__ __device__ inline size_t gq_lds_bytes() { return (size_t)kQSlots * (64 * 4 + 16); }
+__device__ __forceinline__ GQ gq_carve(CTCX_LDS char* p) {
+  GQ q;
+  q.e = (CTCX_LDS uint32_t*)p;
+  q.h = (CTCX_LDS int*)(p + (size_t)kQSlots * 64 * 4);
+  return q;
+}
+
+template <typename T>
+__device__ __forceinline__ void help_gather_chunks(const Ctx<T>& cx, GQ q, int buf, int nb, T norm, T pmax, T bottom) {
+  const int lane = threadIdx.x & 63;
+  CTCX_LDS int* m = cx.misc;
+  if (ctl_ld(m, kCtlDead) != 0) return;
+  const int tsn = cx.rns;
+  const T txo = cx.rxout;
+  int i0 = 0, li0 = 0, cbr = -1;
+  bool gstop = false;
+  for (int c = 0;; ++c) {
+    bool done = false;
+    for (int spin = 0;; ++spin) {   // the grow still running, and a free slot
+      if (ctl_ld(m, kCtlDone) != 0) { done = true; break; }
+      if (spin > kSpinCap) {
+        __hip_atomic_store(&m[kCtlDead], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        done = true;
+        break;
+      }
+      if (c < ctl_ld(m, kCtlCons) + kQSlots) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (done) break;
+    // wave 0's bottom after its last chunk (it only rises)
+    const T pb = (T)__builtin_bit_cast(float, (unsigned)ctl_ld(m, kCtlBot));
+    bottom = pb > bottom ? pb : bottom;
+    const int slot = c % kQSlots;
+    const int s_i0 = i0, s_l0 = li0;
+    int cqn = 0;
+    gather_chunk<T>(cx, buf, nb, norm, pmax, bottom, tsn, txo, i0, li0, cbr, gstop, q.e + slot * 64, cqn, nullptr);
+    if (lane == 0) {
+      q.h[slot * 4 + 0] = cqn;
+      q.h[slot * 4 + 1] = s_i0;
+      q.h[slot * 4 + 2] = s_l0;
+      q.h[slot * 4 + 3] = gstop ? 1 : 0;
+    }
+    __hip_atomic_store(&m[kCtlReady], c + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (cqn == 0 || gstop) break;   // the last chunk of the frame
+  }
+  if (cbr >= 0) cq_children(cx, buf, nb, cbr, -1);   // the child bitmap starts the next frame clear
+}
+
 template <typename T, int RN, bool BIG, class SC, bool HW>
 __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, bool last, int P, int* n_out,
-                          int* n_leaves, uint64_t* pc, Tab tb) {
+                          int* n_leaves, uint64_t* pc, Tab tb, GQ gq) {
   uint64_t ts0 = pc ? __builtin_amdgcn_s_memtime() : 0;
   // HW: both waves run up to the recursion, then wave 1 becomes the helper;
   // wave 0 (threadIdx.x == lane) runs the rest
@@ -1761,15 +2072,21 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
   for (int i = tid; i < nb; i += NT) recurse_branch<T, SC>(cx, buf, i, i, norm, false);
   __syncthreads();
   bool nonfinite = false;
+  T lmin = pinf<T>();   // (the smallest leaf: the bottom of a full beam)
   for (int i = lane; i < nb; i += 64) {   // (HW: each wave tests every branch, so both decide alike)
     const T v = cx.et[i];
     nonfinite |= !(v > NI && v < pinf<T>());
+    lmin = v < lmin ? v : lmin;
     if (!HW || tid < 64) he_st(he, i + 1, HE<T>{v, i});     // leaves_.push(b) in branch order
   }
   if (__ballot(nonfinite)) return 1;
   if constexpr (HW) {
     if (tid >= 64) {
-      help_score_chunks<T>(cx, tb, buf, nb, norm);
+      if constexpr (BIG) {
+        if (nb >= W) help_gather_chunks<T>(cx, gq, buf, nb, norm, pmax, wave_min(lmin));
+      } else {
+        help_score_chunks<T>(cx, tb, buf, nb, norm);
+      }
       return 0;   // the kernel takes wave 0's result
     }
   } else {
@@ -1825,6 +2142,8 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
   // a closed turn found by the gather, the branch whose children the bitmap holds
   int cqn = 0, cq_i0 = 0, cq_l0 = 0, cbr = -1;
   bool gstop = false;
+  int gqc = 0;               // HW, large C: chunks taken from the gather queue
+  uint32_t gqe = 0, gqp = 0; // ... this chunk's entry of the lane and of the lane before
   // |S|, the row's top set, and the largest value outside S (pre-pass; for
   // double rows |S| = 0 and the S path below is never taken)
   const int tsn = BIG ? cx.rns : 0;
@@ -2198,234 +2517,37 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     // grow ends after this chunk) and again in the chunk at the bottom its turn
     // sees (sl, bat below).
     if (BIG && full) {
-      CTCX_LDS uint32_t* cq = row_cq(cx);
-      CTCX_LDS uint64_t* cbm = row_cbm(cx);
-      CTCX_LDS uint64_t* cwin = cbm + (Cm1 + 63) / 64;
-      cq_i0 = i0;
-      cq_l0 = li0;
-      cqn = 0;
-      // the branch scan (lane j: branch sb + j) and a branch's window scan
-      // (lane w: window wa0 + w) hold for the whole gather: no event moves the
-      // bottom before the chunk runs
-      int sb = -1, wa0 = -1;
-      uint64_t hitM = 0, brkM = 0, chM = 0, wkM = 0;
-      T otb = NI, ot0 = NI;
-      bool enter = true;   // at the gather's start or a branch's first offer
-      const uint64_t tg0 = pc ? __builtin_amdgcn_s_memtime() : 0;
-      const T tsx = lane < tsn ? (T)row_topx(cx)[lane] : NI;                          // S in label-index order:
-      const int tsl = lane < tsn ? ((CTCX_LDS int*)(row_topx(cx) + kTopK))[lane] : Cm1;   // lane j its j-th
-      while (cqn < 64) {
-        const uint64_t te0 = pc ? __builtin_amdgcn_s_memtime() : 0;
-        if (enter) {
-          // the next branch with a turn closed (stop), or with something to
-          // gather (pmax + ot > bottom, or children)
-          int res = 0;   // 0: at a branch to gather from, 1: a turn is closed, 2: past the last branch
-          for (;;) {
-            if (sb < 0 || i0 >= sb + 64) {
-              sb = i0;
-              const int ib = i0 + lane;
-              bool brk = false, skp = true, ch = false;
-              otb = NI;
-              if (ib < nb) {
-                otb = sel(cx.ot, buf)[ib];
-                ch = cx.head[ib] >= 0;
-                brk = (lane > 0 || li0 == 0) && !(otb > bottom);
-                skp = !(pmax + otb > bottom) && !ch;
-              }
-              hitM = __ballot(brk || !skp);
-              brkM = __ballot(brk);
-              chM = __ballot(ch);
-            }
-            const uint64_t m = hitM & ~lowmask(i0 - sb);
-            if (m == 0) {
-              i0 = sb + 64;
-              li0 = 0;
-              if (i0 >= nb) { res = 2; break; }
-              continue;
-            }
-            const int k = (int)__builtin_ctzll(m);
-            if (sb + k > i0) li0 = 0;
-            i0 = sb + k;
-            if ((brkM >> k) & 1ull) res = 1;
-            ot0 = bcast(otb, k);
-            const int nbr = ((chM >> k) & 1ull) ? i0 : -1;
-            if (nbr != cbr) {
-              cq_children(cx, buf, nb, cbr, nbr);
-              cbr = nbr;
-            }
+      if constexpr (HW) {
+        // the next chunk of wave 1's gather queue (the published count is read
+        // first, so the reads issued after it see the chunk)
+        const int slot = gqc % kQSlots;
+        int h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+        for (int spin = 0;; ++spin) {
+          const int rdy = __hip_atomic_load(&cx.misc[kCtlReady], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __asm__ volatile("" ::: "memory");
+          h0 = gq.h[slot * 4 + 0]; h1 = gq.h[slot * 4 + 1]; h2 = gq.h[slot * 4 + 2]; h3 = gq.h[slot * 4 + 3];
+          gqe = gq.e[slot * 64 + lane];
+          gqp = gq.e[slot * 64 + (lane > 0 ? lane - 1 : 0)];
+          if (uni(rdy) > gqc || cx.tabdead) break;
+          if (spin > kSpinCap) {   // never in a correct run: give up for the rest of the kernel
+            cx.tabdead = 1;
+            __hip_atomic_store(&cx.misc[kCtlDead], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             break;
           }
-          if (pc) pc[20] += __builtin_amdgcn_s_memtime() - te0;
-          if (res == 1) gstop = true;
-          if (res != 0) break;
-          if (pc) pc[21] += 1;
-          enter = false;
-          wa0 = -1;
+          __builtin_amdgcn_s_sleep(1);
         }
-        if (tsn > 0 && !(((txo - norm) + ot0) > bottom)) {
-          if (pc) pc[22] += 1;
-          if (li0 == 0 && cbr != i0) {
-            // a run of branches i0, i0 + 1, ... (lane L: branch i0 + L) each
-            // with every candidate in S, no branch children and an open turn
-            // (branch i0's was checked by the branch scan): each takes one
-            // ballot of its S offers that beat the bound, in branch order,
-            // while they fit the chunk -- the same decisions and entries as
-            // the per-branch path below, without its branch selection
-            const int ib = i0 + lane;
-            const bool vb = ib < nb;
-            const T otL = vb ? sel(cx.ot, buf)[ib] : NI;
-            const bool okL = vb && (otL > bottom) && cx.head[ib] < 0 && !(((txo - norm) + otL) > bottom);
-            const uint64_t badM = ~__ballot(okL || lane == 0);
-            const int R = badM ? (int)__builtin_ctzll(badM) : 64;   // run length (>= 1)
-            const T sxv = tsx - norm;                                // S lane j: x_j - norm
-            int L = 0;
-            for (; L < R; ++L) {
-              const T ob = bcast(otL, L);
-              const bool h = lane < tsn && ((sxv + ob) > bottom);
-              const uint64_t hM = __ballot(h);
-              const int nh = __builtin_popcountll(hM);
-              if (nh > 64 - cqn) break;
-              if (h) {
-                const int r = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(hM >> 32),
-                                                             __builtin_amdgcn_mbcnt_lo((unsigned)hM, 0u));
-                cq[cqn + r] = ((uint32_t)(i0 + L) << 16) | (uint32_t)tsl;
-              }
-              cqn += nh;
-            }
-            if (L > 0) {
-              i0 += L;
-              li0 = 0;
-              enter = true;
-              if (i0 >= nb) break;
-              continue;
-            }
-          }
-          // every candidate of branch i0 is in S: its offers from li0 on that
-          // beat the bound, merged in label order with its children (from the
-          // bitmap, ascending); a branch that does not fit the chunk's room
-          // starts the next chunk (or, first in the chunk, goes by windows)
-          const bool hot = tsl >= li0 && (((tsx - norm) + ot0) > bottom);
-          const uint64_t hotM = __ballot(hot);
-          const int nh = __builtin_popcountll(hotM);
-          int padd = 0, nch = 0;
-          if (cbr == i0) {
-            for (int q = 0; q * 64 < (Cm1 + 63) / 64; ++q) {
-              uint64_t wq = uni64(cwin[q]);
-              while (wq) {
-                const int a = q * 64 + (int)__builtin_ctzll(wq);
-                wq &= wq - 1ull;
-                uint64_t bits = uni64(cbm[a]);
-                if (a * 64 < li0) bits &= ~lowmask(li0 - a * 64);
-                while (bits) {
-                  const int xc = a * 64 + (int)__builtin_ctzll(bits);
-                  bits &= bits - 1ull;
-                  if (__ballot(hot && tsl == xc)) continue;   // also a hot offer of S
-                  const int pos = cqn + __builtin_popcountll(hotM & __ballot(tsl < xc)) + nch;
-                  if (lane == 0 && pos < 64) cq[pos] = ((uint32_t)i0 << 16) | (uint32_t)xc;
-                  padd += (tsl > xc) ? 1 : 0;
-                  ++nch;
-                }
-              }
-            }
-          }
-          if (pc) pc[23] += __builtin_amdgcn_s_memtime() - te0;
-          if (nh + nch <= 64 - cqn) {
-            if (hot) {
-              const int r = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(hotM >> 32),
-                                                           __builtin_amdgcn_mbcnt_lo((unsigned)hotM, 0u));
-              cq[cqn + r + padd] = ((uint32_t)i0 << 16) | (uint32_t)tsl;
-            }
-            cqn += nh + nch;
-            ++i0;
-            li0 = 0;
-            enter = true;
-            if (i0 >= nb) break;
-            continue;
-          }
-          if (cqn > 0) break;
-        }
-        // branch i0's aligned 64-label windows from li0 on (lane w: window
-        // wa0 + w): one whose labels' block maxima bound every score
-        // (xb - norm) + ot0 <= bottom and that holds no child is passed over
-        const uint64_t tw0 = pc ? __builtin_amdgcn_s_memtime() : 0;
-        if (pc) pc[17] += 1;
-        if (wa0 < 0 || (li0 >> 6) >= wa0 + 64) {
-          wa0 = li0 >> 6;
-          const int lw = (wa0 + lane) * 64;
-          bool keep = false;
-          if (lw < Cm1) {
-            const int le = (lw + 64 < Cm1 ? lw + 64 : Cm1) - 1;
-            const int la = lw + (lw >= blank ? 1 : 0);
-            const int lb = le + (le >= blank ? 1 : 0);
-            const T ba = bmax[la >> 6], bb = bmax[lb >> 6];
-            const T xb = ba > bb ? ba : bb;
-            const int a = wa0 + lane;
-            keep = (((xb - norm) + ot0) > bottom) || (((cwin[a >> 6] >> (a & 63)) & 1ull) != 0);
-          }
-          wkM = __ballot(keep);
-        }
-        uint64_t m = wkM & ~lowmask((li0 >> 6) - wa0);
-        int nli0;
-        if (m == 0) {
-          nli0 = (wa0 + 64) * 64;
-        } else {
-          // up to kGatherWin kept windows per batch of row reads: the exact
-          // per-label bound, and the children
-          int aw[kGatherWin];
-          T xv[kGatherWin];
-          uint64_t cw[kGatherWin];
-#pragma unroll
-          for (int j = 0; j < kGatherWin; ++j) {
-            aw[j] = -1;
-            if (m) {
-              aw[j] = wa0 + (int)__builtin_ctzll(m);
-              m &= m - 1ull;
-            }
-          }
-#pragma unroll
-          for (int j = 0; j < kGatherWin; ++j) {
-            xv[j] = NI;
-            cw[j] = 0ull;
-            if (aw[j] >= 0) {
-              const int x = aw[j] * 64 + lane;
-              const int xc = x < Cm1 ? x : Cm1 - 1;
-              xv[j] = cx.row[xc + (xc >= blank ? 1 : 0)];
-              cw[j] = cbm[aw[j]];
-            }
-          }
-          nli0 = -1;
-          int endw = 0;
-#pragma unroll
-          for (int j = 0; j < kGatherWin; ++j) {
-            if (aw[j] >= 0 && nli0 < 0 && cqn < 64) {
-              const int wb = aw[j] * 64;
-              const int x = wb + lane;
-              const bool hot = x >= li0 && x < Cm1 &&
-                               ((((xv[j] - norm) + ot0) > bottom) || (((cw[j] >> lane) & 1ull) != 0));
-              uint64_t hotM = __ballot(hot);
-              const int rank =
-                  (int)__builtin_amdgcn_mbcnt_hi((unsigned)(hotM >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)hotM, 0u));
-              if (__builtin_popcountll(hotM) > 64 - cqn) {   // the chunk fills here
-                hotM = __ballot(hot && rank < 64 - cqn);
-                nli0 = wb + 64 - __builtin_clzll(hotM);
-              }
-              if ((hotM >> lane) & 1ull) cq[cqn + rank] = ((uint32_t)i0 << 16) | (uint32_t)x;
-              cqn += __builtin_popcountll(hotM);
-              endw = wb + 64;
-            }
-          }
-          if (nli0 < 0) nli0 = endw;
-        }
-        li0 = nli0;
-        if (pc) pc[18] += __builtin_amdgcn_s_memtime() - tw0;
-        if (li0 >= Cm1) {
-          ++i0;
-          li0 = 0;
-          enter = true;
-          if (i0 >= nb) break;
-        }
+        __asm__ volatile("" ::: "memory");
+        ++gqc;
+        __hip_atomic_store(&cx.misc[kCtlCons], gqc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        cqn = cx.tabdead ? 0 : uni(h0);
+        cq_i0 = uni(h1);
+        cq_l0 = uni(h2);
+        gstop = uni(h3) != 0;
+      } else {
+        cq_i0 = i0;
+        cq_l0 = li0;
+        gather_chunk<T>(cx, buf, nb, norm, pmax, bottom, tsn, txo, i0, li0, cbr, gstop, row_cq(cx), cqn, pc);
       }
-      if (pc) pc[16] += __builtin_amdgcn_s_memtime() - tg0;
       if (cqn == 0) {
         if (gstop) stop = true;
         break;
@@ -2442,10 +2564,16 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       // the compacted chunk: lane j < cqn holds the j-th gathered offer; a
       // branch turn starts at the first lane of its branch unless the branch
       // began before the span
-      CTCX_LDS uint32_t* cq = row_cq(cx);
       valid = lane < cqn;
-      const uint32_t e = cq[valid ? lane : 0];
-      const uint32_t ep = cq[lane > 0 ? lane - 1 : 0];
+      uint32_t e, ep;
+      if constexpr (HW) {
+        e = valid ? gqe : (uint32_t)__builtin_amdgcn_readfirstlane(gqe);   // (read with the slot's header)
+        ep = gqp;
+      } else {
+        CTCX_LDS uint32_t* cq = row_cq(cx);
+        e = cq[valid ? lane : 0];
+        ep = cq[lane > 0 ? lane - 1 : 0];
+      }
       i = (int)(e >> 16);
       li = (int)(e & 0xFFFFu);
       const int ip = lane > 0 ? (int)(ep >> 16) : -1;
@@ -2851,6 +2979,10 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       if constexpr (SC::kStateful) cx.eest[myslot] = cst;
       if (isbc) __hip_atomic_fetch_and(&cx.bst[c], ~S_EVICT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+    if constexpr (HW && BIG)   // the helper gathers the next chunks against this bottom
+      if (full)
+        __hip_atomic_store(&cx.misc[kCtlBot], (int)__builtin_bit_cast(unsigned, (float)bottom), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
     if (pc) pc[15] += __builtin_amdgcn_s_memtime() - q5;
     if (pc) pc[9] += __builtin_amdgcn_s_memtime() - tc1;
   }
@@ -3325,7 +3457,7 @@ __device__ void ring_flush(const Ring<RT>& g, RT* out, int32_t* foff, int t_new,
 // work is thread 0's (wave 0, the decoding wave).
 template <typename T, int RN, int WC, bool BIG, class SC, bool HW>
 __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T> prm) {
-  static_assert(!HW || (sizeof(T) == 4 && RN == 1 && WC == 128 && !BIG && !SC::kStateful), "HW kernels");
+  static_assert(!HW || (sizeof(T) == 4 && !SC::kStateful && (BIG ? WC > 0 : (RN == 1 && WC == 128))), "HW kernels");
   constexpr int NT = HW ? 128 : 64;
   Ctx<T> cx;
 #ifdef CTCX_GSTATE
@@ -3353,15 +3485,20 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
   // HW kernels: 4-byte records, the score table after the decode layout,
   // then the ring, whose flushes the helper wave runs
   const int R = prm.ring;
-  using RT = typename std::conditional<HW, Rec32, Rec>::type;
+  using RT = typename std::conditional<HW && !BIG, Rec32, Rec>::type;
   Ring<RT> rg{};
   Tab tb{};
+  GQ gq{};
 #ifndef CTCX_GSTATE
   {
     size_t off = (decode_lds_bytes(WC > 0 ? WC : W, C, (int)sizeof(T), SC::kStateful) + 15) & ~(size_t)15;
-    if constexpr (HW) {
+    if constexpr (HW && !BIG) {
       tb = tab_carve((CTCX_LDS char*)lds + off);
       off += tab_lds_bytes();
+    }
+    if constexpr (HW && BIG) {
+      gq = gq_carve((CTCX_LDS char*)lds + off);
+      off += gq_lds_bytes();
     }
     if (R > 0) rg = ring_carve<RT>((CTCX_LDS char*)lds + off, R, W);
   }
@@ -3416,8 +3553,10 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
 #else
     for (int j = tid; j < C; j += NT) cx.row[j] = xr[j];
 #endif
-    if constexpr (HW)
-      if (tid < 3) cx.misc[kCtlReady + tid] = 0;   // the helper's hand-over counters, per frame
+    if constexpr (HW) {   // the helper's hand-over words, per frame
+      if (tid < 3) cx.misc[kCtlReady + tid] = 0;
+      if (tid == 3) cx.misc[kCtlBot] = (int)0xff800000u;   // -inf
+    }
     const T norm = prm.norm[(int64_t)t * B + b];
     if constexpr (BIG) {
       // the pre-pass record of row (t, b): header, block maxima, top set
@@ -3448,7 +3587,7 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
     if (prof) pc[0] += t1 - t0;
 #ifndef CTCX_GSTATE   // the global-state tier replays every frame literally
     if (!prm.force_literal && !dup)
-      why = exact_step<T, RN, BIG, SC, HW>(cx, buf, nb, norm, last, prm.P, &n, &nl_fast, prof ? pc : nullptr, tb);
+      why = exact_step<T, RN, BIG, SC, HW>(cx, buf, nb, norm, last, prm.P, &n, &nl_fast, prof ? pc : nullptr, tb, gq);
 #endif
     if constexpr (HW) {
       // wave 0's result for both waves; the helper stops if the grow ended
@@ -3460,7 +3599,7 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
         cx.misc[6] = nl_fast;
       }
       if (tid >= 64 && pf_t >= 0)   // the helper: the flush the previous commit left pending
-        ring_flush<2, RT, true>(rg, rstream, foff, pf_t, pf_lo, pf_hi, nullptr, 0, pf_fp, nrec);
+        ring_flush<(WC > 0 ? WC : 512) / 64, RT, true>(rg, rstream, foff, pf_t, pf_lo, pf_hi, nullptr, 0, pf_fp, nrec);
       pf_t = -1;
       __syncthreads();
       why = uni(cx.misc[4]);
@@ -3661,8 +3800,8 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
   // stream cursor is then the item's record count)
   if constexpr (HW) {
     if (R > 0 && sl > 0 && tid >= 64) {
-      if (pf_t >= 0) ring_flush<2, RT, true>(rg, rstream, foff, pf_t, pf_lo, pf_hi, nullptr, 0, pf_fp, nrec);
-      ring_flush<2, RT, true>(rg, rstream, foff, sl - 1, flushed, sl - 1, cx.tops, np, nflush, nrec);
+      if (pf_t >= 0) ring_flush<(WC > 0 ? WC : 512) / 64, RT, true>(rg, rstream, foff, pf_t, pf_lo, pf_hi, nullptr, 0, pf_fp, nrec);
+      ring_flush<(WC > 0 ? WC : 512) / 64, RT, true>(rg, rstream, foff, sl - 1, flushed, sl - 1, cx.tops, np, nflush, nrec);
       if (tid == 64) misc[13] = nrec;
     }
     __syncthreads();
@@ -4325,7 +4464,7 @@ template <typename T, int RN, int WC, bool BIG, class SC, bool HW = false>
 hipError_t launch_decode_c(const DecodeParams<T>& p, hipStream_t s) {
   // the decode layout, then (HW) the score table, then the record ring
   size_t lds = decode_lds_bytes(WC > 0 ? WC : p.W, p.C, (int)sizeof(T), SC::kStateful);
-  if (HW) lds = ((lds + 15) & ~(size_t)15) + tab_lds_bytes();
+  if (HW) lds = ((lds + 15) & ~(size_t)15) + (BIG ? gq_lds_bytes() : tab_lds_bytes());
   if (p.ring > 0) lds = ((lds + 15) & ~(size_t)15) + ring_lds_bytes(p.ring, p.W, HW ? 4 : 8);
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)ctcx_beam_decode<T, RN, WC, BIG, SC, HW>,
@@ -4378,6 +4517,7 @@ hipError_t launch_decode_c(const DecodeParams<T>& p, hipStream_t s) {
 #define CTCX_IF_6(...)
 #define CTCX_IF_7(...)
 #define CTCX_IF_8(...)
+#define CTCX_IF_10(...)
 #if CTCX_PART == 1
 #undef CTCX_IF_1
 #define CTCX_IF_1(...) __VA_ARGS__
@@ -4402,6 +4542,9 @@ hipError_t launch_decode_c(const DecodeParams<T>& p, hipStream_t s) {
 #elif CTCX_PART == 8
 #undef CTCX_IF_8
 #define CTCX_IF_8(...) __VA_ARGS__
+#elif CTCX_PART == 10
+#undef CTCX_IF_10
+#define CTCX_IF_10(...) __VA_ARGS__
 #endif
 #define CTCX_IF_PART(P, ...) CTCX_IF_##P(__VA_ARGS__)
 #if CTCX_PART == 0
@@ -4413,13 +4556,21 @@ hipError_t launch_decode_c(const DecodeParams<T>& p, hipStream_t s) {
 #endif
 CTCX_DECODE_INSTANCES(CTCX_X)
 #undef CTCX_X
-// the two-wave (helper) kernel of the cfg2/cfg3 class, part 8
+// the two-wave (helper) kernels: the cfg2/cfg3 class (part 8), large C (part 10)
 #if CTCX_PART == 0
 extern template hipError_t launch_decode_c<float, 1, 128, false, BaseBeamScorer<float>, true>(
+    const DecodeParams<float>&, hipStream_t);
+extern template hipError_t launch_decode_c<float, 1, 128, true, BaseBeamScorer<float>, true>(
+    const DecodeParams<float>&, hipStream_t);
+extern template hipError_t launch_decode_c<float, 2, 256, true, BaseBeamScorer<float>, true>(
     const DecodeParams<float>&, hipStream_t);
 #else
 CTCX_IF_PART(8, template hipError_t launch_decode_c<float, 1, 128, false, BaseBeamScorer<float>, true>(
                     const DecodeParams<float>&, hipStream_t);)
+CTCX_IF_PART(10, template hipError_t launch_decode_c<float, 1, 128, true, BaseBeamScorer<float>, true>(
+                     const DecodeParams<float>&, hipStream_t);)
+CTCX_IF_PART(10, template hipError_t launch_decode_c<float, 2, 256, true, BaseBeamScorer<float>, true>(
+                     const DecodeParams<float>&, hipStream_t);)
 #endif
 
 #if CTCX_PART == 0
@@ -4431,31 +4582,37 @@ static hipError_t launch_decode_r(const DecodeParams<T>& p, hipStream_t s) {
   return p.C > 64 ? launch_decode_c<T, RN, WC, true, SC>(p, s) : launch_decode_c<T, RN, WC, false, SC>(p, s);
 }
 
-// float, beams <= 128, C <= 64, the base scorer, no record ring: the two-wave
-// kernel, which writes 4-byte records (CTCEXT_HELPER=0, diagnostics: the
-// one-wave kernel instead)
+// The two-wave kernels (helper_kind; 0: none): 1 the score table (float,
+// beams <= 128, C <= 64; 4-byte records), 2 the gather queue (float, beams <=
+// 256, C > 64).  The base scorer only.  CTCEXT_HELPER=0 (diagnostics): the
+// one-wave kernels instead.
 template <typename T>
-bool helper_shape(const DecodeParams<T>& p) {
-  if (sizeof(T) != 4 || p.scorer_tab != nullptr || p.W > kRec32MaxBeam || p.C > kRec32MaxClasses) return false;
+int helper_kind(const DecodeParams<T>& p) {
+  if (sizeof(T) != 4 || p.scorer_tab != nullptr) return 0;
   const char* hv = getenv("CTCEXT_HELPER");
-  return !(hv && hv[0] == '0');
+  if (hv && hv[0] == '0') return 0;
+  if (p.C <= kRec32MaxClasses) return p.W <= kRec32MaxBeam ? 1 : 0;
+  return p.W <= 256 ? 2 : 0;
 }
-// LDS bytes before the record ring: the decode layout and, for the two-wave
-// kernel, its score table
+__host__ inline int helper_wc(int W) { return W <= 128 ? 128 : 256; }
+// LDS bytes before the record ring: the decode layout and the helper's table
+// or gather queue
 template <typename T>
-size_t pre_ring_lds_bytes(const DecodeParams<T>& p, bool hw, int wc) {
-  size_t b = (decode_lds_bytes(wc, p.C, (int)sizeof(T), p.scorer_tab != nullptr) + 15) & ~(size_t)15;
-  return hw ? b + tab_lds_bytes() : b;
+size_t pre_ring_lds_bytes(const DecodeParams<T>& p, int hk, int wc) {
+  const size_t b = (decode_lds_bytes(wc, p.C, (int)sizeof(T), p.scorer_tab != nullptr) + 15) & ~(size_t)15;
+  return hk == 1 ? b + tab_lds_bytes() : hk == 2 ? b + gq_lds_bytes() : b;
 }
+// the two-wave kernel this call runs (0: none): its layout and ring must fit
 template <typename T>
-bool use_helper_kernel(const DecodeParams<T>& p) {
-  if (!helper_shape(p)) return false;
-  size_t b = pre_ring_lds_bytes(p, true, 128);
-  if (p.ring > 0) b = ((b + 15) & ~(size_t)15) + ring_lds_bytes(p.ring, p.W, 4);
-  return b <= kLdsBytes;
+int use_helper_kernel(const DecodeParams<T>& p) {
+  const int hk = helper_kind(p);
+  if (hk == 0) return 0;
+  size_t b = pre_ring_lds_bytes(p, hk, helper_wc(p.W));
+  if (p.ring > 0) b = ((b + 15) & ~(size_t)15) + ring_lds_bytes(p.ring, p.W, hk == 1 ? 4 : 8);
+  return b <= kLdsBytes ? hk : 0;
 }
-template bool use_helper_kernel<float>(const DecodeParams<float>&);
-template bool use_helper_kernel<double>(const DecodeParams<double>&);
+template int use_helper_kernel<float>(const DecodeParams<float>&);
+template int use_helper_kernel<double>(const DecodeParams<double>&);
 
 template <typename T>
 hipError_t launch_decode(const DecodeParams<T>& p, hipStream_t s) {
@@ -4470,8 +4627,13 @@ hipError_t launch_decode(const DecodeParams<T>& p, hipStream_t s) {
     return launch_decode_r<T, 4, 0, SC>(p, s);
   }
   auto fits = [&](int wc) { return decode_lds_bytes(wc, p.C, (int)sizeof(T), false) <= kLdsBytes; };
-  if constexpr (sizeof(T) == 4)
-    if (use_helper_kernel(p)) return launch_decode_c<float, 1, 128, false, BaseBeamScorer<float>, true>(p, s);
+  if constexpr (sizeof(T) == 4) {
+    const int hk = use_helper_kernel(p);
+    if (hk == 1) return launch_decode_c<float, 1, 128, false, BaseBeamScorer<float>, true>(p, s);
+    if (hk == 2)
+      return p.W <= 128 ? launch_decode_c<float, 1, 128, true, BaseBeamScorer<float>, true>(p, s)
+                        : launch_decode_c<float, 2, 256, true, BaseBeamScorer<float>, true>(p, s);
+  }
   if (p.W <= 128) return fits(128) ? launch_decode_r<T, 1, 128>(p, s) : launch_decode_r<T, 1, 0>(p, s);
   if (p.W <= 256) return fits(256) ? launch_decode_r<T, 2, 256>(p, s) : launch_decode_r<T, 2, 0>(p, s);
   return launch_decode_r<T, 4, 0>(p, s);
@@ -4491,10 +4653,12 @@ int ring_frames(const DecodeParams<T>& p, int cus, int cap) {
   auto fits = [&](int wc) { return decode_lds_bytes(wc, p.C, (int)sizeof(T), scored) <= kLdsBytes; };
   const int wcap = (p.W <= 128 && fits(128)) ? 128 : (p.W > 128 && p.W <= 256 && fits(256)) ? 256 : p.W;
   if ((int64_t)p.Tmax * p.W > 0x7fffffffLL) return 0;
-  // the two-wave kernel (when its layout and a ring fit): table + 4-byte records
-  const bool hw = helper_shape(p) && pre_ring_lds_bytes(p, true, 128) + ring_lds_bytes(8, p.W, 4) <= kLdsBytes;
-  const int rb = hw ? 4 : 8;
-  const size_t base = pre_ring_lds_bytes(p, hw, hw ? 128 : wcap);
+  // the two-wave kernel, when its layout and a ring fit (the score table's
+  // records are 4 bytes)
+  int hk = helper_kind(p);
+  if (hk && pre_ring_lds_bytes(p, hk, helper_wc(p.W)) + ring_lds_bytes(8, p.W, hk == 1 ? 4 : 8) > kLdsBytes) hk = 0;
+  const int rb = hk == 1 ? 4 : 8;
+  const size_t base = pre_ring_lds_bytes(p, hk, hk ? helper_wc(p.W) : wcap);
   const size_t budget = (base > 80 * 1024 || p.B <= cus) ? kLdsBytes : 80 * 1024;
   // the kernel addresses ring rows by t & (R - 1): R must be a power of two
   if (cap < 8) return 0;
