@@ -120,6 +120,7 @@ struct Dev {
   int64_t lo = 0, nb = 0;    // this call's shard [lo, lo + nb)
   int ring = 0;              // this call's record-ring frames (ctcx::ring_frames)
   int rec_bytes = 8;         // this call's record size (8, 16 or 4 bytes)
+  int helper = 0;            // this call's two-wave kernel (ctcx::use_helper_kernel)
   int cus = 0;               // compute units of the device
 };
 
@@ -449,7 +450,8 @@ static int enqueue_shard(ctcext_decoder* d, Dev& v, bool root, const ctcext_deco
   tp.rec = p.rec; tp.item = p.item; tp.seq_len = sl; tp.top_pos = p.top_pos; tp.top_kind = p.top_kind;
   tp.Tmax = T_; tp.B = Bs; tp.W = W; tp.P = P; tp.merge = a->merge_repeated ? 1 : 0;
   tp.blank_label = a->blank_label;
-  tp.rec_fmt = gs ? ctcx::kRecFmt128 : ctcx::use_helper_kernel<T>(p) == 1 ? ctcx::kRecFmt32 : ctcx::kRecFmt64;
+  v.helper = gs ? 0 : ctcx::use_helper_kernel<T>(p);
+  tp.rec_fmt = gs ? ctcx::kRecFmt128 : v.helper == 1 ? ctcx::kRecFmt32 : ctcx::kRecFmt64;
   v.rec_bytes = tp.rec_fmt == ctcx::kRecFmt128 ? 16 : tp.rec_fmt == ctcx::kRecFmt32 ? 4 : 8;
   tp.foff = p.foff;
   tp.seq = (int32_t*)v.seq.p;
@@ -555,6 +557,7 @@ static int run_decode(ctcext_decoder* d, const ctcext_decode_args* a, const std:
   d->stats.tier = use_gstate(a) ? 1 : 0;
   d->stats.ring_frames = root.ring;
   d->stats.record_bytes = root.rec_bytes;
+  d->stats.helper = root.helper;
   if (a->flags & CTCEXT_FLAG_PROFILE) {
     for (int i = 0; i < nd; ++i) {
       Dev& v = d->devs[(size_t)i];

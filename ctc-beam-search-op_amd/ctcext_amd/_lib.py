@@ -72,7 +72,7 @@ class Stats(ctypes.Structure):
                 ("traceback_ms", ctypes.c_double), ("n_devices", ctypes.c_int32),
                 ("tier", ctypes.c_int32), ("ring_frames", ctypes.c_int32),
                 ("records_written", ctypes.c_int64), ("record_bytes", ctypes.c_int32),
-                ("pad_", ctypes.c_int32)]
+                ("helper", ctypes.c_int32)]
 
 
 _lib = None

@@ -128,7 +128,8 @@ typedef struct {
   int32_t record_bytes;            /* last decode: bytes per record (8; 16 on the global-state
                                       tier; 4 in the two-wave kernel, beam_width <= 128 and
                                       num_classes <= 64) */
-  int32_t pad_;
+  int32_t helper;                  /* last decode: the two-wave kernel that ran (0: the one-wave
+                                      kernel; 1: score-table helper; 2: gather-queue helper) */
 } ctcext_stats;
 
 /* Handle lifetime.  A handle owns a HIP stream and a grow-only device

@@ -643,3 +643,39 @@ def test_record_ring_matches_direct_records():
                      "alignment_indices", "alignment_values", "alignment_shape"):
             np.testing.assert_array_equal(to_numpy(getattr(a, name)[p]), to_numpy(getattr(b, name)[p]))
     np.testing.assert_array_equal(to_numpy(a.log_probability), to_numpy(b.log_probability))
+
+
+# ---- the two-wave kernels (ctcx_decode.hip help_score_chunks, the score
+# table: float, beams <= 128, C <= 64; help_gather_chunks, the gather queue:
+# float, beams <= 256, C > 64) are the default for the base scorer, and every
+# family above runs through them; the one-wave kernels stay the path for the
+# other shapes and are forced here (CTCEXT_HELPER=0) on the same families
+
+
+def test_helper_kernel_selection():
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal((20, 2, 29)).astype(np.float32)
+    ctcext_amd.ctc_ext_beam_search_decoder(x, [20, 20], 16, 1)
+    assert _stats()["helper"] == 1 and _stats()["record_bytes"] == 4
+    x2 = rng.standard_normal((20, 2, 300)).astype(np.float32)
+    ctcext_amd.ctc_ext_beam_search_decoder(x2, [20, 20], 200, 1)
+    assert _stats()["helper"] == 2 and _stats()["record_bytes"] == 8
+    ctcext_amd.ctc_ext_beam_search_decoder(x.astype(np.float64), [20, 20], 16, 1)
+    assert _stats()["helper"] == 0
+    ctcext_amd.ctc_ext_beam_search_decoder(x, [20, 20], 300, 1)
+    assert _stats()["helper"] == 0
+
+
+@pytest.fixture
+def one_wave(monkeypatch):
+    monkeypatch.setenv("CTCEXT_HELPER", "0")
+
+
+def test_one_wave_kernels_random_families(one_wave):
+    _run_random(9101, 60)
+    assert _stats()["helper"] == 0 and _stats()["record_bytes"] == 8
+    _run_random(9102, 40, ties=True)
+    _run_random(9103, 15, T_max=30, B_max=2, C_min=65, C_max=300, W_max=100)
+    _run_random(9104, 30, flags=RMIN)
+    _run_random(9105, 10, T_max=40, B_max=2, C_min=3, C_max=40, W_min=129, W_max=256)
+    _run_random(9106, 8, T_max=30, B_max=2, C_min=65, C_max=500, W_min=129, W_max=256, ties=True)
