@@ -1562,7 +1562,7 @@ __device__ __forceinline__ void cq_children(const Ctx<T>& cx, int buf, int nb, i
   CTCX_LDS uint64_t* cbm = row_cbm(cx);
   CTCX_LDS uint64_t* cwin = cbm + (cx.C - 1 + 63) / 64;
   if (ob >= 0) {
-    for (int k = threadIdx.x; k < nb; k += 64) {
+    for (int k = (int)(threadIdx.x & 63); k < nb; k += 64) {   // (also run by the two-wave kernels' helper)
       const int pk = sel(cx.par, buf)[k];
       const int lk = sel(cx.lab, buf)[k];
       if (pk == ob) {
@@ -1573,7 +1573,7 @@ __device__ __forceinline__ void cq_children(const Ctx<T>& cx, int buf, int nb, i
     }
   }
   if (nb_ >= 0) {
-    for (int k = threadIdx.x; k < nb; k += 64) {
+    for (int k = (int)(threadIdx.x & 63); k < nb; k += 64) {
       const int pk = sel(cx.par, buf)[k];
       const int lk = sel(cx.lab, buf)[k];
       if (pk == nb_) {

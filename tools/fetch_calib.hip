@@ -17,6 +17,8 @@
 //                    different XCDs)
 //   calib_rec_store  the decode kernel's record store: 8 B per lane, W = 128
 //                    records per (item, frame) (cfg3: 393 MB)
+//   calib_rec32_store  the two-wave kernel's 4-byte records: 4 B per thread,
+//                    128 threads per item, one record each per frame
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -58,6 +60,14 @@ __global__ __launch_bounds__(64) void calib_rec_store(unsigned long long* __rest
   }
 }
 
+__global__ __launch_bounds__(128) void calib_rec32_store(unsigned* __restrict__ rec, int T, int W) {
+  const int b = blockIdx.x, k = threadIdx.x;
+  for (int t = 0; t < T; ++t) {
+    unsigned* r = rec + ((size_t)b * T + t) * W;
+    if (k < W) r[k] = ((unsigned)t << 8) | (unsigned)k;
+  }
+}
+
 int main() {
   const int T = 1500, B = 256, C = 29, W = 128;
   const size_t n = (size_t)T * B * C;
@@ -79,9 +89,11 @@ int main() {
     CK(hipDeviceSynchronize());
     hipLaunchKernelGGL(calib_rec_store, dim3(B), dim3(64), 0, 0, rec, T, W);
     CK(hipDeviceSynchronize());
+    hipLaunchKernelGGL(calib_rec32_store, dim3(B), dim3(128), 0, 0, (unsigned*)rec, T, W);
+    CK(hipDeviceSynchronize());
   }
-  printf("{\"calib_stream16\": %zu, \"calib_rows\": %zu, \"calib_rec_store_write\": %zu}\n", bytes / 16 * 16, bytes,
-         (size_t)B * T * W * 8);
+  printf("{\"calib_stream16\": %zu, \"calib_rows\": %zu, \"calib_rec_store_write\": %zu, "
+         "\"calib_rec32_store_write\": %zu}\n", bytes / 16 * 16, bytes, (size_t)B * T * W * 8, (size_t)B * T * W * 4);
   free(h);
   return 0;
 }

@@ -46,10 +46,14 @@ def main():
     write, nw, _ = per_launch(write_csv, "WRITE_SIZE", "ctcx_beam_decode")
     c_rows, _, _ = per_launch(cf_csv, "FETCH_SIZE", "calib_rows")
     c_s16, _, _ = per_launch(cf_csv, "FETCH_SIZE", "calib_stream16")
-    c_rec, _, _ = per_launch(cw_csv, "WRITE_SIZE", "calib_rec_store")
+    # the decode kernel's record width: REC_BYTES=4 for the two-wave kernel
+    # (stats.record_bytes), else the 8-byte records
+    rb = int(os.environ.get("REC_BYTES", "8"))
+    cname, kname = ("calib_rec32_store", "calib_rec32_store_write") if rb == 4 else ("calib_rec_store", "calib_rec_store_write")
+    c_rec, _, _ = per_launch(cw_csv, "WRITE_SIZE", cname)
     f_rows = known["calib_rows"] / (c_rows * 1024)
     f_s16 = known["calib_stream16"] / (c_s16 * 1024)
-    f_rec = known["calib_rec_store_write"] / (c_rec * 1024)
+    f_rec = known[kname] / (c_rec * 1024)
     rd = fetch * 1024 * f_rows
     wr = write * 1024 * f_rec
     with open(LIB, "rb") as f:
@@ -58,7 +62,7 @@ def main():
         "config": cfg, "seq_len": int(seq_len), "kernel": name, "lib_sha16": sha,
         "fetch_size_kb_raw": fetch, "write_size_kb_raw": write, "launches": [nf, nw],
         "calibration": {"fetch_factor_rows_4B_lane": f_rows, "fetch_factor_stream_16B_lane": f_s16,
-                        "write_factor_records_8B_lane": f_rec, "tool": "tools/fetch_calib.hip"},
+                        "write_factor_records": f_rec, "record_bytes": rb, "tool": "tools/fetch_calib.hip"},
         "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
         "hbm_bytes_per_launch": rd + wr,
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "

@@ -26,7 +26,7 @@ timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch_ca
 step write-calib
 timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write_calib -o run -- $R/tools/fetch_calib > /dev/null 2> $O/write_calib.log || exit 15
 cc() { find $1 -name '*counter_collection.csv' | head -1; }
-python3 $R/tools/pmc_summary.py $(cc $O/fetch_cfg3) $(cc $O/write_cfg3) cfg3 1500 $(cc $O/fetch_calib) $(cc $O/write_calib) $O/calib.json > $O/pmc_cfg3.json || exit 16
+REC_BYTES=${REC_BYTES:-4} python3 $R/tools/pmc_summary.py $(cc $O/fetch_cfg3) $(cc $O/write_cfg3) cfg3 1500 $(cc $O/fetch_calib) $(cc $O/write_calib) $O/calib.json > $O/pmc_cfg3.json || exit 16
 cp $O/pmc_cfg3.json $R/profiles/pmc_cfg3.json
 step bench-cfg3
 cd $R
