@@ -2228,7 +2228,10 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
           const int need = c + 2 < nch ? c + 2 : nch;
           u32x4 ta[2];
           float tpv[2];
+          const uint64_t tq0 = pc ? __builtin_amdgcn_s_memtime() : 0;
+          int spins = 0;
           for (int spin = 0;; ++spin) {
+            spins = spin;
             const int rdy = __hip_atomic_load(&cx.misc[kCtlReady], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             __asm__ volatile("" ::: "memory");
             const int s0 = (c % kTabSlots) * 64 + lane, s1 = ((c + 1) % kTabSlots) * 64 + lane;
@@ -2246,6 +2249,11 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
           }
           __asm__ volatile("" ::: "memory");
           __hip_atomic_store(&cx.misc[kCtlCons], c + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (pc) {   // diagnostics: the table wait (its s_sleep rounds)
+            (void)uni((int)ta[1].x);
+            pc[19] += __builtin_amdgcn_s_memtime() - tq0;
+            pc[20] += spins;
+          }
           int wi[2], wl[2], slw[2], cw[2], bsti[2], cst[2];
           bool wv[2], wlive[2];
           T sw[2], bt[2], batw[2];
@@ -3788,6 +3796,13 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
     __syncthreads();
     if (prof) { pc[4] += __builtin_amdgcn_s_memtime() - t3; pc[7] += 1; }
   }
+#ifdef CTCX_PHASES
+  if constexpr (HW) {   // diagnostics: where the two waves ran (HW_ID: SIMD in bits 5:4, CU in 11:8)
+    if (tid == 64) misc[14] = (int)__builtin_amdgcn_s_getreg(63492);
+    __syncthreads();
+    if (prof) { pc[21] = (uint64_t)__builtin_amdgcn_s_getreg(63492); pc[22] = (uint64_t)(uint32_t)misc[14]; }
+  }
+#endif
   if (prof && tid == 0)
     for (int q = 0; q < kPhaseN; ++q) prm.prof[b * kPhaseN + q] = pc[q];
 
@@ -4465,7 +4480,7 @@ hipError_t launch_decode_c(const DecodeParams<T>& p, hipStream_t s) {
   // the decode layout, then (HW) the score table, then the record ring
   size_t lds = decode_lds_bytes(WC > 0 ? WC : p.W, p.C, (int)sizeof(T), SC::kStateful);
   if (HW) lds = ((lds + 15) & ~(size_t)15) + (BIG ? gq_lds_bytes() : tab_lds_bytes());
-  if (p.ring > 0) lds = ((lds + 15) & ~(size_t)15) + ring_lds_bytes(p.ring, p.W, HW ? 4 : 8);
+  if (p.ring > 0) lds = ((lds + 15) & ~(size_t)15) + ring_lds_bytes(p.ring, p.W, HW && !BIG ? 4 : 8);
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)ctcx_beam_decode<T, RN, WC, BIG, SC, HW>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

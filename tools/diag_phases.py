@@ -43,3 +43,13 @@ for b in o[-3:][::-1]:
     print("    item %d: heap events %.0f/frame, extract %.0f, grow %.0f, eventloop %.0f, scoring %.0f" % (
         b, buf[b, 6] / fr, buf[b, 3] / fr, buf[b, 2] / fr, buf[b, 9] / fr, buf[b, 8] / fr))
 print("  mean heap events/frame %.1f, max %.1f" % (buf[:, 6].mean() / fr, buf[:, 6].max() / fr))
+# two-wave kernels (cfg2/cfg3 class): the score-table wait and where the waves ran
+if len(sys.argv) <= 5 or int(sys.argv[5]) <= 64:
+    print("  HW table wait %.0f cycles/frame, %.2f s_sleep rounds/frame" % (m[19] / fr, m[20] / fr))
+    w0, w1 = buf[:, 21].astype(np.int64), buf[:, 22].astype(np.int64)
+    simd0, simd1 = (w0 >> 4) & 3, (w1 >> 4) & 3
+    cu0, cu1 = (w0 >> 8) & 15, (w1 >> 8) & 15
+    same_cu = (cu0 == cu1) & (((w0 >> 13) & 3) == ((w1 >> 13) & 3)) & (((w0 >> 12) & 1) == ((w1 >> 12) & 1))
+    print("  HW waves: same CU %d/%d items, same SIMD %d/%d items (wave0 SIMD histogram %s, helper %s)" % (
+        int(same_cu.sum()), B, int((same_cu & (simd0 == simd1)).sum()), B,
+        np.bincount(simd0, minlength=4).tolist(), np.bincount(simd1, minlength=4).tolist()))
