@@ -1620,7 +1620,13 @@ __device__ __forceinline__ void wsync() {
     __syncthreads();
   }
 }
-constexpr int kTabSlots = 16;          // chunk slots in the ring
+#ifndef CTCX_TAB_SLOTS
+#define CTCX_TAB_SLOTS 16
+#endif
+#ifndef CTCX_SLEEP
+#define CTCX_SLEEP 1
+#endif
+constexpr int kTabSlots = CTCX_TAB_SLOTS;   // chunk slots in the ring
 constexpr int kSpinCap = 1 << 16;      // s_sleep(1) rounds before a wait gives up (~4 ms)
 struct Tab {
   CTCX_LDS u32x4* a;    // [slot][lane]: score, branch total, packed, candidate back-pointer
@@ -1664,7 +1670,7 @@ __device__ __forceinline__ void help_score_chunks(const Ctx<T>& cx, Tab tb, int 
       const int cons = ctl_ld(m, kCtlCons);
       c = c > cons ? c : cons;   // chunks wave 0 has passed are never read
       if (c < cons + kTabSlots) break;
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(CTCX_SLEEP);
     }
     if (c >= nch) return;
     const int o = 64 * c + lane;
@@ -2002,7 +2008,7 @@ __device__ __forceinline__ void help_gather_chunks(const Ctx<T>& cx, GQ q, int b
         break;
       }
       if (c < ctl_ld(m, kCtlCons) + kQSlots) break;
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(CTCX_SLEEP);
     }
     if (done) break;
     // wave 0's bottom after its last chunk (it only rises)
@@ -2142,6 +2148,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
   // a closed turn found by the gather, the branch whose children the bitmap holds
   int cqn = 0, cq_i0 = 0, cq_l0 = 0, cbr = -1;
   bool gstop = false;
+  bool dz = false;           // a branch was deactivated this frame (HW window loop: bst then read)
   int gqc = 0;               // HW, large C: chunks taken from the gather queue
   uint32_t gqe = 0, gqp = 0; // ... this chunk's entry of the lane and of the lane before
   // |S|, the row's top set, and the largest value outside S (pre-pass; for
@@ -2181,6 +2188,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
             const int kc = bcast(cw[H], k);                                                                         \
             if (!((gtM >> k) & 1ull)) {                                                                             \
               evr = writelane(evr, kc | kDeactRec, nv);                                                             \
+              dz = true;                                                             \
               nv += 1;                                                                                              \
               const uint64_t dm0 = ~__ballot(wi[0] == kc), dm1 = ~__ballot(wi[1] == kc);                            \
               NCw[0] &= dm0; LBw[0] &= dm0; RBw[0] &= dm0;                                                          \
@@ -2230,22 +2238,38 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
           float tpv[2];
           const uint64_t tq0 = pc ? __builtin_amdgcn_s_memtime() : 0;
           int spins = 0;
-          for (int spin = 0;; ++spin) {
-            spins = spin;
+          const int s0 = (c % kTabSlots) * 64 + lane, s1 = ((c + 1) % kTabSlots) * 64 + lane;
+          {
+            // one batch of reads, no loop around it (a loop would make the
+            // compiler wait out every read's predecessor: write-after-write on
+            // the same registers across the back edge)
             const int rdy = __hip_atomic_load(&cx.misc[kCtlReady], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             __asm__ volatile("" ::: "memory");
-            const int s0 = (c % kTabSlots) * 64 + lane, s1 = ((c + 1) % kTabSlots) * 64 + lane;
             ta[0] = tb.a[s0];
             tpv[0] = tb.p[s0];
             ta[1] = tb.a[s1];
             tpv[1] = tb.p[s1];
-            if (uni(rdy) >= need || cx.tabdead) break;
-            if (spin > kSpinCap) {   // never in a correct run: give up for the rest of the kernel
-              cx.tabdead = 1;
-              __hip_atomic_store(&cx.misc[kCtlDead], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-              break;
+            // the slot reads complete with the count (one round trip): otherwise
+            // the compiler sinks them below the test, a second round trip
+            __asm__ volatile("" ::"v"(ta[0]), "v"(ta[1]), "v"(tpv[0]), "v"(tpv[1]));
+            if (__builtin_expect(uni(rdy) < need && !cx.tabdead, 0)) {
+              // wave 1 is behind (rare): wait for the count, then read again
+              for (int spin = 0;; ++spin) {
+                spins = spin + 1;
+                __builtin_amdgcn_s_sleep(CTCX_SLEEP);
+                if (ctl_ld(cx.misc, kCtlReady) >= need) break;
+                if (spin > kSpinCap) {   // never in a correct run: give up for the rest of the kernel
+                  cx.tabdead = 1;
+                  __hip_atomic_store(&cx.misc[kCtlDead], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                  break;
+                }
+              }
+              __asm__ volatile("" ::: "memory");
+              ta[0] = tb.a[s0];
+              tpv[0] = tb.p[s0];
+              ta[1] = tb.a[s1];
+              tpv[1] = tb.p[s1];
             }
-            __builtin_amdgcn_s_sleep(1);
           }
           __asm__ volatile("" ::: "memory");
           __hip_atomic_store(&cx.misc[kCtlCons], c + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2276,11 +2300,17 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
             stM[h] = __ballot(wv[h] && wli == 0 && lane + 64 * h != 0);
           }
           if (turnw && !(bcast(bt[0], 0) > bottom)) break;   // branch i0's turn: skipped, and all later
-          // what events change: the offer's branch deactivated, its branch child evicted
+          // what events change: the offer's branch deactivated (read only after a
+          // deactivation this frame), its branch child evicted (read only when
+          // the window re-offers a branch child: a few windows per frame)
+          bsti[0] = bsti[1] = cst[0] = cst[1] = 0;
+          if (dz) {
   #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            bsti[h] = cx.bst[wi[h]];
-            cst[h] = cx.bst[cw[h] >= 0 ? cw[h] : wi[h]];
+            for (int h = 0; h < 2; ++h) bsti[h] = cx.bst[wi[h]];
+          }
+          if (__ballot(cw[0] >= 0 || cw[1] >= 0)) {
+  #pragma unroll
+            for (int h = 0; h < 2; ++h) cst[h] = cx.bst[cw[h] >= 0 ? cw[h] : wi[h]];
           }
           uint64_t NCw[2], LBw[2], RBw[2], donew[2] = {0ull, 0ull};
   #pragma unroll
@@ -2530,19 +2560,29 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
         // first, so the reads issued after it see the chunk)
         const int slot = gqc % kQSlots;
         int h0 = 0, h1 = 0, h2 = 0, h3 = 0;
-        for (int spin = 0;; ++spin) {
+        {
+          // one batch of reads, no loop around it (see the score-table read)
           const int rdy = __hip_atomic_load(&cx.misc[kCtlReady], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           __asm__ volatile("" ::: "memory");
           h0 = gq.h[slot * 4 + 0]; h1 = gq.h[slot * 4 + 1]; h2 = gq.h[slot * 4 + 2]; h3 = gq.h[slot * 4 + 3];
           gqe = gq.e[slot * 64 + lane];
           gqp = gq.e[slot * 64 + (lane > 0 ? lane - 1 : 0)];
-          if (uni(rdy) > gqc || cx.tabdead) break;
-          if (spin > kSpinCap) {   // never in a correct run: give up for the rest of the kernel
-            cx.tabdead = 1;
-            __hip_atomic_store(&cx.misc[kCtlDead], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            break;
+          __asm__ volatile("" ::"v"(h0), "v"(h1), "v"(h2), "v"(h3), "v"(gqe), "v"(gqp));   // one round trip
+          if (__builtin_expect(uni(rdy) <= gqc && !cx.tabdead, 0)) {
+            for (int spin = 0;; ++spin) {   // wave 1 is behind: wait for the count, then read again
+              __builtin_amdgcn_s_sleep(CTCX_SLEEP);
+              if (ctl_ld(cx.misc, kCtlReady) > gqc) break;
+              if (spin > kSpinCap) {   // never in a correct run: give up for the rest of the kernel
+                cx.tabdead = 1;
+                __hip_atomic_store(&cx.misc[kCtlDead], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                break;
+              }
+            }
+            __asm__ volatile("" ::: "memory");
+            h0 = gq.h[slot * 4 + 0]; h1 = gq.h[slot * 4 + 1]; h2 = gq.h[slot * 4 + 2]; h3 = gq.h[slot * 4 + 3];
+            gqe = gq.e[slot * 64 + lane];
+            gqp = gq.e[slot * 64 + (lane > 0 ? lane - 1 : 0)];
           }
-          __builtin_amdgcn_s_sleep(1);
         }
         __asm__ volatile("" ::: "memory");
         ++gqc;
@@ -2722,7 +2762,8 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
             const int kc = bcast(c, k);
             if (!((gtM >> k) & 1ull)) {
               // re-offered evicted branch rejected -> deactivated (decoder.h:200-205)
-              evr = writelane(evr, kc | kDeactRec, nv);
+              evr = writelane(evr, kc | kDeactRec, nv);                                                             \
+              dz = true;
               nv += 1;
               const uint64_t dm = ~__ballot(i == kc);
               NC &= dm; LB &= dm; RB &= dm;
@@ -2773,6 +2814,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
               if (!((gtM >> k) & 1ull)) {
                 // re-offered evicted branch rejected -> deactivated (decoder.h:200-205)
                 evr = writelane(evr, slot | kDeactRec, nv);
+                dz = true;
                 nv += 1;
                 const uint64_t dm = ~__ballot(i == slot);
                 NC &= dm; LB &= dm; RB &= dm;
@@ -2855,6 +2897,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
               const int k_c = bcast(c, k);
               // re-offered evicted branch rejected -> deactivated (decoder.h:200-205)
               evr = (lane == nev) ? (k_c | kDeactRec) : evr;
+              dz = true;
               nev += 1;
               liveM &= ~__ballot(i == k_c);
               continue;
@@ -2956,6 +2999,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       } else {
         // re-offered evicted branch rejected -> deactivated (decoder.h:200-205)
         evr = (lane == nev) ? (k_c | kDeactRec) : evr;
+              dz = true;
         nev += 1;
         live = live && (i != k_c);
       }
@@ -3483,6 +3527,11 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int64_t b = blockIdx.x;
+#ifdef CTCX_PRIO
+  if constexpr (HW) {   // the decoding wave first
+    if (__builtin_amdgcn_readfirstlane(tid) < 64) __builtin_amdgcn_s_setprio(3);   // (a scalar branch)
+  }
+#endif
   const int W = prm.W;
   const int C = (int)prm.C;
   const int64_t B = prm.B;
