@@ -2278,16 +2278,15 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
             pc[19] += __builtin_amdgcn_s_memtime() - tq0;
             pc[20] += spins;
           }
-          int wi[2], wl[2], slw[2], cw[2], bsti[2], cst[2];
-          bool wv[2], wlive[2];
+          // per-lane fields, then every per-lane predicate as a wave mask (SGPRs)
+          int wi[2], wl[2], slw[2], cw[2];
           T sw[2], bt[2], batw[2];
           Best<T> cdw[2];
-          uint64_t stM[2], wantM[2];
+          uint64_t wvM[2], stM[2], bcM[2], wantM[2];
   #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const unsigned x = (h == 0 || c + 1 < nch) ? (unsigned)ta[h].z : 0u;
             const unsigned a0 = ta[h].x, a1 = ta[h].y, a3 = ta[h].w;
-            wv[h] = ((x >> 27) & 1u) != 0u;
             wi[h] = (int)(x & 127u);
             wl[h] = (int)((x >> 7) & 63u);
             const int wli = (int)((x >> 13) & 63u);
@@ -2297,32 +2296,31 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
             cdw[h] = Best<T>{(T)tpv[h], a3, true};
             slw[h] = lane + 64 * h - wli;   // window position where the lane's branch turn starts
             batw[h] = slw[h] > 0 ? bottom : NI;
-            stM[h] = __ballot(wv[h] && wli == 0 && lane + 64 * h != 0);
+            wvM[h] = __ballot((x >> 27) & 1u);
+            bcM[h] = __ballot((x >> 19) & 255u);   // the offer re-offers a branch child
+            stM[h] = wvM[h] & __ballot(wli == 0) & (h == 0 ? ~1ull : ~0ull);
           }
           if (turnw && !(bcast(bt[0], 0) > bottom)) break;   // branch i0's turn: skipped, and all later
           // what events change: the offer's branch deactivated (read only after a
           // deactivation this frame), its branch child evicted (read only when
           // the window re-offers a branch child: a few windows per frame)
-          bsti[0] = bsti[1] = cst[0] = cst[1] = 0;
+          uint64_t dM[2] = {0ull, 0ull}, eM[2] = {0ull, 0ull};
           if (dz) {
   #pragma unroll
-            for (int h = 0; h < 2; ++h) bsti[h] = cx.bst[wi[h]];
+            for (int h = 0; h < 2; ++h) dM[h] = __ballot(cx.bst[wi[h]] & S_DEACT);
           }
-          if (__ballot(cw[0] >= 0 || cw[1] >= 0)) {
+          if (bcM[0] | bcM[1]) {
   #pragma unroll
-            for (int h = 0; h < 2; ++h) cst[h] = cx.bst[cw[h] >= 0 ? cw[h] : wi[h]];
+            for (int h = 0; h < 2; ++h) eM[h] = bcM[h] & __ballot(cx.bst[cw[h] >= 0 ? cw[h] : wi[h]] & S_EVICT);
           }
           uint64_t NCw[2], LBw[2], RBw[2], donew[2] = {0ull, 0ull};
   #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            wlive[h] = wv[h] && !(bsti[h] & S_DEACT);
-            const bool isbc = cw[h] >= 0;
-            const bool cev = isbc && (cst[h] & S_EVICT) != 0;
-            wantM[h] = __ballot(wlive[h] && (isbc ? cev : (sw[h] > bottom)));
-            const uint64_t liveM = __ballot(wlive[h]), isbm = __ballot(isbc);
-            NCw[h] = liveM & ~isbm;
-            LBw[h] = liveM & isbm;
-            RBw[h] = LBw[h] & __ballot(cev);
+            const uint64_t liveM = wvM[h] & ~dM[h];
+            NCw[h] = liveM & ~bcM[h];
+            LBw[h] = liveM & bcM[h];
+            RBw[h] = LBw[h] & eM[h];
+            wantM[h] = (NCw[h] & __ballot(sw[h] > bottom)) | RBw[h];
           }
           if (pc) pc[10] += __builtin_amdgcn_s_memtime() - tc0;
           if (!(wantM[0] | wantM[1])) {
@@ -2350,7 +2348,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
           bottom = fv;
           nextfree = nfree;
           // the turn continuing into the next window: skipped -> so is every later one
-          if ((__ballot(wv[1] && !(bt[1] > batw[1])) >> 63) & 1ull) stop = true;
+          if (((wvM[1] & ~__ballot(bt[1] > batw[1])) >> 63) & 1ull) stop = true;
           const uint64_t q5 = pc ? __builtin_amdgcn_s_memtime() : 0;
           if (lane < nv) {
             const int rs = evr & ~kDeactRec;
