@@ -51,7 +51,6 @@ constexpr int F_HN = 8;      // has a label-ending alignment candidate
 // per-frame branch state bits
 constexpr int S_EVICT = 1;   // pushed this frame, then evicted from the beam
 constexpr int S_DEACT = 2;   // deactivated (oldp reset): grows no children
-constexpr int S_READD = 4;   // two-wave kernels: the branch's entry was evicted and re-added this frame
 constexpr int kDeactRec = 1 << 30;   // exact_step chunk record: deactivation (else eviction)
 
 template <typename T> __host__ __device__ __forceinline__ T ninf();
@@ -1629,58 +1628,26 @@ __device__ __forceinline__ void wsync() {
 #endif
 constexpr int kTabSlots = CTCX_TAB_SLOTS;   // chunk slots in the ring
 constexpr int kSpinCap = 1 << 16;      // s_sleep(1) rounds before a wait gives up (~4 ms)
-// The accepted offers' entries are staged as their raw table words, by entry
-// slot (sa, sp); wave 1 writes the entry arrays from them after the grow
-// (tab_materialize), while wave 0 extracts.
-constexpr int kStageSlots = 3 * 128 + 2;   // the entry capacity at beams <= 128
 struct Tab {
   CTCX_LDS u32x4* a;    // [slot][lane]: score, branch total, packed, candidate back-pointer
   CTCX_LDS float* p;    // [slot][lane]: candidate value
-  CTCX_LDS u32x4* sa;   // [entry slot]: the accepted offer's table words
-  CTCX_LDS float* sp;   // [entry slot]: ... its candidate value
 };
-__host__ __device__ inline size_t tab_lds_bytes() { return (size_t)kTabSlots * 64 * 20 + (size_t)kStageSlots * 20 + 8; }
+__host__ __device__ inline size_t tab_lds_bytes() { return (size_t)kTabSlots * 64 * 20; }
 __device__ __forceinline__ Tab tab_carve(CTCX_LDS char* p) {
   Tab t;
   t.a = (CTCX_LDS u32x4*)p;
   t.p = (CTCX_LDS float*)(p + (size_t)kTabSlots * 64 * 16);
-  t.sa = (CTCX_LDS u32x4*)(p + (size_t)kTabSlots * 64 * 20);
-  t.sp = (CTCX_LDS float*)(p + (size_t)kTabSlots * 64 * 20 + (size_t)kStageSlots * 16);
   return t;
 }
 // control words in misc[8..11]; kCtlDead (sticky for the kernel): a wait gave
 // up, every later wait returns at once, and the item reports it (ItemOut.pad)
 constexpr int kCtlReady = 8, kCtlCons = 9, kCtlDone = 10, kCtlDead = 11;
-// kCtlDone: 1 the grow ended (wave 1 then writes the staged entries), 2 the
-// same, but wave 0 writes them itself (it reads them at once: the last
-// frame's TopPaths, a std::sort Extract), 3 the frame left the fast path
-// (nothing to write); kCtlFree: the bump pointer at the grow's end
-constexpr int kCtlFree = 15;
 __device__ __forceinline__ int ctl_ld(CTCX_LDS int* m, int k) {
   return uni(__hip_atomic_load(&m[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
 }
 // packed: branch (bits 0-6), label (7-12), label index (13-18), branch child + 1 (19-26), valid (27)
 __device__ __forceinline__ unsigned tab_pack(int i, int l, int li, int cw, bool v) {
   return (unsigned)i | ((unsigned)l << 7) | ((unsigned)li << 13) | ((unsigned)(cw + 1) << 19) | (v ? 1u << 27 : 0u);
-}
-
-// The entries of the offers accepted this frame, from their staged table
-// words: the slots past the branches' (new children, [nb, nf)) and the
-// branches' own re-added entries (S_READD).  Threads tid0, tid0 + NT, ...
-template <typename T>
-__device__ __forceinline__ void tab_materialize(const Ctx<T>& cx, Tab tb, int nb, int nf, int tid0, int NT) {
-  for (int e = tid0; e < nf; e += NT) {
-    if (e < nb && !(cx.bst[e] & S_READD)) continue;
-    const u32x4 w = tb.sa[e];
-    const unsigned sc = w.x, x = w.z, bp = w.w;
-    const T v = (T)__builtin_bit_cast(float, sc);
-    const int i = (int)(x & 127u), l = (int)((x >> 7) & 63u), cw = (int)((x >> 19) & 255u) - 1;
-    cx.et[e] = v; cx.eb[e] = ninf<T>(); cx.el[e] = v;
-    cx.ecn[e] = (T)tb.sp[e]; cx.ebpn[e] = bp;
-    cx.eflg[e] = F_HN;
-    cx.ekind[e] = cw >= 0 ? ((uint32_t)cw << 1) : (((uint32_t)i << 1) | 1u);
-    cx.elab[e] = l;
-  }
 }
 
 template <typename T>
@@ -1693,10 +1660,9 @@ __device__ __forceinline__ void help_score_chunks(const Ctx<T>& cx, Tab tb, int 
   const int nch = (nb * Cm1 + 63) >> 6;
   CTCX_LDS int* m = cx.misc;
   if (ctl_ld(m, kCtlDead) != 0) return;
-  bool quit = false;
-  for (int c = 0; c < nch && !quit; ++c) {
+  for (int c = 0; c < nch; ++c) {
     for (int spin = 0;; ++spin) {   // the grow still running, and a free slot
-      if (ctl_ld(m, kCtlDone) != 0) { quit = true; break; }
+      if (ctl_ld(m, kCtlDone) != 0) return;
       if (spin > kSpinCap) {
         __hip_atomic_store(&m[kCtlDead], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         return;
@@ -1706,7 +1672,7 @@ __device__ __forceinline__ void help_score_chunks(const Ctx<T>& cx, Tab tb, int 
       if (c < cons + kTabSlots) break;
       __builtin_amdgcn_s_sleep(CTCX_SLEEP);
     }
-    if (quit || c >= nch) break;
+    if (c >= nch) return;
     const int o = 64 * c + lane;
     int q = (int)((float)o * rcp);
     q -= (q * Cm1 > o) ? 1 : 0;
@@ -1751,18 +1717,6 @@ __device__ __forceinline__ void help_score_chunks(const Ctx<T>& cx, Tab tb, int 
     tb.p[slot] = (float)cd.p;
     __hip_atomic_store(&m[kCtlReady], c + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
-  // the grow's end, then (kCtlDone == 1) the staged entries
-  int dn = 0;
-  for (int spin = 0;; ++spin) {
-    dn = ctl_ld(m, kCtlDone);
-    if (dn != 0) break;
-    if (spin > kSpinCap) {
-      __hip_atomic_store(&m[kCtlDead], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      return;
-    }
-    __builtin_amdgcn_s_sleep(CTCX_SLEEP);
-  }
-  if (dn == 1) tab_materialize<T>(cx, tb, nb, ctl_ld(m, kCtlFree), lane, 64);
 }
 
 // large C, the beam full: one compacted chunk.  The offers of the span from
@@ -2409,13 +2363,14 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
   #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const int ms = mys[h];
-            if (ms >= 0) {   // staged: wave 1 writes the entry after the grow (tab_materialize)
-              tb.sa[ms] = ta[h];
-              tb.sp[ms] = tpv[h];
-              if (cw[h] >= 0) {
-                __hip_atomic_fetch_and(&cx.bst[cw[h]], ~S_EVICT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                __hip_atomic_fetch_or(&cx.bst[cw[h]], S_READD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-              }
+            if (ms >= 0) {
+              const bool isbc = cw[h] >= 0;
+              cx.et[ms] = sw[h]; cx.eb[ms] = NI; cx.el[ms] = sw[h];
+              cx.ecn[ms] = cdw[h].p; cx.ebpn[ms] = cdw[h].bp;
+              cx.eflg[ms] = F_HN;
+              cx.ekind[ms] = isbc ? ((uint32_t)cw[h] << 1) : (((uint32_t)wi[h] << 1) | 1u);
+              cx.elab[ms] = wl[h];
+              if (isbc) __hip_atomic_fetch_and(&cx.bst[cw[h]], ~S_EVICT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
           }
           if (pc) pc[15] += __builtin_amdgcn_s_memtime() - q5;
@@ -3066,23 +3021,12 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       }
     }
     if (myslot >= 0) {
-      if constexpr (HW && !BIG) {   // staged as a table entry (tab_materialize)
-        u32x4 w;
-        w.x = __builtin_bit_cast(unsigned, (float)s);
-        w.y = 0u;
-        w.z = tab_pack(i, l, li, c, true);
-        w.w = cd.bp;
-        tb.sa[myslot] = w;
-        tb.sp[myslot] = (float)cd.p;
-        if (isbc) __hip_atomic_fetch_or(&cx.bst[c], S_READD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      } else {
-        cx.et[myslot] = s; cx.eb[myslot] = NI; cx.el[myslot] = s;
-        cx.ecn[myslot] = cd.p; cx.ebpn[myslot] = cd.bp;
-        cx.eflg[myslot] = F_HN;
-        cx.ekind[myslot] = isbc ? ((uint32_t)c << 1) : (((uint32_t)i << 1) | 1u);
-        cx.elab[myslot] = l;
-        if constexpr (SC::kStateful) cx.eest[myslot] = cst;
-      }
+      cx.et[myslot] = s; cx.eb[myslot] = NI; cx.el[myslot] = s;
+      cx.ecn[myslot] = cd.p; cx.ebpn[myslot] = cd.bp;
+      cx.eflg[myslot] = F_HN;
+      cx.ekind[myslot] = isbc ? ((uint32_t)c << 1) : (((uint32_t)i << 1) | 1u);
+      cx.elab[myslot] = l;
+      if constexpr (SC::kStateful) cx.eest[myslot] = cst;
       if (isbc) __hip_atomic_fetch_and(&cx.bst[c], ~S_EVICT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     if constexpr (HW && BIG)   // the helper gathers the next chunks against this bottom
@@ -3093,23 +3037,8 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     if (pc) pc[9] += __builtin_amdgcn_s_memtime() - tc1;
   }
 
-  // the grow is over: the helper stops scoring (and writes the staged entries,
-  // except in the last frame, whose TopPaths reads them at once)
-  if constexpr (HW) {
-    if constexpr (!BIG) {
-      // wave 0 writes them itself when it reads them next: the last frame's
-      // TopPaths, and the std::sort Extract of a frame whose beam never filled
-      const bool self = last || st != kTopHeap;
-      if (lane == 0) cx.misc[kCtlFree] = nextfree;
-      __hip_atomic_store(&cx.misc[kCtlDone], self ? 2 : 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (self) {
-        tab_materialize<T>(cx, tb, nb, nextfree, lane, 64);
-        wsync<HW>();
-      }
-    } else {
-      __hip_atomic_store(&cx.misc[kCtlDone], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-  }
+  // the grow is over: the helper stops scoring
+  if constexpr (HW) __hip_atomic_store(&cx.misc[kCtlDone], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   if (BIG && cbr >= 0) cq_children(cx, buf, nb, cbr, -1);
   uint64_t ts2 = pc ? __builtin_amdgcn_s_memtime() : 0;
   if (pc) pc[2] += ts2 - ts1;
@@ -3719,8 +3648,7 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
       // wave 0's result for both waves; the helper stops if the grow ended
       // early (a frame handed to the literal path)
       if (tid == 0) {
-        if (why != 0)   // the frame left the fast path (the grow's end, if reached, set 1 or 2)
-          __hip_atomic_store(&cx.misc[kCtlDone], 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(&cx.misc[kCtlDone], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         cx.misc[4] = why;
         cx.misc[5] = n;
         cx.misc[6] = nl_fast;
