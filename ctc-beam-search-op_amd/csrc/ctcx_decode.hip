@@ -3606,7 +3606,34 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
 #ifdef CTCX_GSTATE
     cx.row = const_cast<T*>(xr);
 #else
-    for (int j = tid; j < C; j += NT) cx.row[j] = xr[j];
+    if constexpr (BIG && sizeof(T) == 4) {
+      // a large row: 16-byte loads, a batch of them in flight per thread
+      // before the first LDS write (a load-store pair per element waited out
+      // one global latency each: 16k cycles per cfg5 frame)
+      if ((C & 3) == 0 && (((uintptr_t)xr) & 15) == 0) {
+        const u32x4* x4 = (const u32x4*)xr;
+        CTCX_LDS u32x4* r4 = (CTCX_LDS u32x4*)cx.row;
+        const int C4 = C >> 2;
+        constexpr int kRB = 8;
+        for (int q0 = 0; q0 < C4; q0 += kRB * NT) {
+          u32x4 v[kRB];
+  #pragma unroll
+          for (int u = 0; u < kRB; ++u) {
+            const int q = q0 + u * NT + tid;
+            if (q < C4) v[u] = x4[q];
+          }
+  #pragma unroll
+          for (int u = 0; u < kRB; ++u) {
+            const int q = q0 + u * NT + tid;
+            if (q < C4) r4[q] = v[u];
+          }
+        }
+      } else {
+        for (int j = tid; j < C; j += NT) cx.row[j] = xr[j];
+      }
+    } else {
+      for (int j = tid; j < C; j += NT) cx.row[j] = xr[j];
+    }
 #endif
     if constexpr (HW) {   // the helper's hand-over words, per frame
       if (tid < 3) cx.misc[kCtlReady + tid] = 0;
