@@ -303,11 +303,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    kms, lit = [], 0
+    kms, lit, pms, tms = [], 0, [], []
     for _ in range(args.steps):
         out = step()
         st = dec.last_stats
         kms.append(st["decode_kernel_ms"])
+        pms.append(st["norm_kernel_ms"])
+        tms.append(st["traceback_ms"])
         lit += st["literal_frames"]
     torch.cuda.synchronize()
     if world > 1:
@@ -359,7 +361,10 @@ def main():
                      # 4 in the two-wave kernel; with the LDS record ring only those
                      # the traceback can reach)
                      "record_ring_frames": st["ring_frames"], "records_written": st["records_written"],
-                     "record_bytes": st["record_bytes"]},
+                     "record_bytes": st["record_bytes"], "helper_kernel": st["helper"],
+                     # the other kernels of the call (HIP events): the row pre-pass
+                     # (normaliser; large C also the row facts) and traceback + pack
+                     "prepass_ms": float(np.mean(pms)), "traceback_ms": float(np.mean(tms))},
         "literal_frames_per_step": lit / max(args.steps, 1),
         "lib_sha16": lib_hash(),
         "what": ("one decode call: device logits in, int64 SparseTensor components materialised on the host"
