@@ -237,7 +237,10 @@ def main():
     ap.add_argument("--scorer", choices=["base", "bigram"], default="base",
                     help="diagnostics: the bigram beam scorer with a random <= 0 table (not a bench line)")
     ap.add_argument("--record-ring", action="store_true",
-                    help="diagnostics: the LDS record ring (only reachable beam records written to HBM)")
+                    help="diagnostics: ask for the LDS record ring (only reachable beam records written to HBM; "
+                         "the default where the score-table two-wave kernel runs)")
+    ap.add_argument("--no-ring", action="store_true",
+                    help="diagnostics: every beam record to HBM (no record ring)")
     ap.add_argument("--no-strong", action="store_true",
                     help="skip the strong-scaling extra (N=1: the per-GPU latency at the B=256/N shards; "
                          "N>1: the measured global-B=256 split)")
@@ -277,7 +280,8 @@ def main():
     sl = torch.as_tensor(sl_np, device=dev)
     torch.cuda.synchronize()
 
-    flags = _lib.CTCEXT_FLAG_PROFILE | (_lib.CTCEXT_FLAG_RECORD_RING if args.record_ring else 0)
+    flags = (_lib.CTCEXT_FLAG_PROFILE | (_lib.CTCEXT_FLAG_RECORD_RING if args.record_ring else 0)
+             | (_lib.CTCEXT_FLAG_NO_RING if args.no_ring else 0))
     dec = ctcext_amd.get_decoder(local)
     skw = {}
     if args.scorer == "bigram":   # ctc_beam_scorer.h's hook with a bigram table of log-probabilities

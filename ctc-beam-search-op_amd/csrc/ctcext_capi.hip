@@ -28,6 +28,8 @@ int ring_frames(const DecodeParams<T>& p, int cus, int cap);
 template <typename T>
 int use_helper_kernel(const DecodeParams<T>& p);
 template <typename T>
+int helper_kind(const DecodeParams<T>& p);
+template <typename T>
 hipError_t launch_row_norm(const T* x, const int32_t* sl, T* norm, int64_t T_, int64_t B, int64_t C,
                            int64_t xstride, hipStream_t s);
 hipError_t launch_traceback(const TraceParams& tp, hipStream_t s);
@@ -425,7 +427,10 @@ static int enqueue_shard(ctcext_decoder* d, Dev& v, bool root, const ctcext_deco
   if (Bs > 0x7fffffffLL || (!gs && (W > ctcx::kMaxRecBeam || C > ctcx::kMaxRecClasses)))
     return fail(CTCEXT_INTERNAL, "shard shape outside the kernel's limits");
   v.ring = 0;
-  if (!gs && (a->flags & (CTCEXT_FLAG_RECORD_RING | CTCEXT_FLAG_RING_MIN))) {
+  // the record ring: asked for, or the default of the score-table two-wave kernel
+  const bool ring = (a->flags & (CTCEXT_FLAG_RECORD_RING | CTCEXT_FLAG_RING_MIN)) ||
+                    (!(a->flags & CTCEXT_FLAG_NO_RING) && ctcx::helper_kind<T>(p) == 1);
+  if (!gs && ring) {
     if (v.cus == 0 && hipDeviceGetAttribute(&v.cus, hipDeviceAttributeMultiprocessorCount, v.device) != hipSuccess)
       v.cus = 1;
     // CTCEXT_RING_FRAMES (diagnostics): a smaller ring cap than the default 64

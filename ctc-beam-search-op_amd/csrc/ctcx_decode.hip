@@ -4264,11 +4264,15 @@ __global__ __launch_bounds__(64) void ctcx_row_prep(const T* __restrict__ x, con
 // class-order sum spread over 64 rows at a time, the maximum taken from the
 // header written here): the one-lane class-order sum of ctcx_row_prep was the
 // bulk of its time.  Four rows per 256-thread block, one per wave.
+// keys at or above the first bracket's lower end (the smallest lane maximum)
+// kept for the in-register bisection: at C = 5000, N(0,1) rows hold ~270 of
+// them, past ctcx_row_prep's 256 (whose fallback bisects over all C keys)
+constexpr int kFactsCompact = 1024;
 template <int NV>
 __global__ __launch_bounds__(256) void ctcx_row_facts(const float* __restrict__ x,
                                                      const int32_t* __restrict__ seq_len, char* __restrict__ prep,
                                                      int64_t rows, int64_t B, int C, int64_t xstride, int blank) {
-  __shared__ unsigned cks_all[4][kPrepCompact];
+  __shared__ unsigned cks_all[4][kFactsCompact];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t row = (int64_t)blockIdx.x * 4 + wv;
   if (row >= rows) return;   // wave-uniform, and no block barrier below
@@ -4353,7 +4357,7 @@ __global__ __launch_bounds__(256) void ctcx_row_facts(const float* __restrict__ 
     if (km > 0u && ckm == K) {
       lo = km - 1;   // exactly the K largest: tau = km
       hi = km;
-    } else if (km > 0u && ckm <= kPrepCompact) {
+    } else if (km > 0u && ckm <= kFactsCompact) {
       // every key >= km into a compact list, then bisect in registers
       lo = km;
       unsigned* cks = cks_all[wv];
@@ -4371,14 +4375,14 @@ __global__ __launch_bounds__(256) void ctcx_row_facts(const float* __restrict__ 
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      unsigned ck[kPrepCompact / 64];
+      unsigned ck[kFactsCompact / 64];
 #pragma unroll
-      for (int q = 0; q < kPrepCompact / 64; ++q) ck[q] = 64 * q + lane < n ? cks[64 * q + lane] : 0u;
+      for (int q = 0; q < kFactsCompact / 64; ++q) ck[q] = 64 * q + lane < n ? cks[64 * q + lane] : 0u;
       while (hi - lo > 1) {
         const uint64_t mid = (lo + hi) >> 1;
         int c = 0;
 #pragma unroll
-        for (int q = 0; q < kPrepCompact / 64; ++q) c += ck[q] >= (unsigned)mid ? 1 : 0;
+        for (int q = 0; q < kFactsCompact / 64; ++q) c += ck[q] >= (unsigned)mid ? 1 : 0;
         c = uni(wave_sum_dpp(c));
         if (c <= K) hi = mid;
         else lo = mid;
@@ -4702,6 +4706,8 @@ int use_helper_kernel(const DecodeParams<T>& p) {
 }
 template int use_helper_kernel<float>(const DecodeParams<float>&);
 template int use_helper_kernel<double>(const DecodeParams<double>&);
+template int helper_kind<float>(const DecodeParams<float>&);
+template int helper_kind<double>(const DecodeParams<double>&);
 
 template <typename T>
 hipError_t launch_decode(const DecodeParams<T>& p, hipStream_t s) {

@@ -25,6 +25,7 @@ CTCEXT_FLAG_PHASES = 4
 CTCEXT_FLAG_GLOBAL_STATE = 8   # testing: the global-state tier whatever the shape
 CTCEXT_FLAG_RECORD_RING = 16   # beam records kept in an LDS ring; only the reachable ones written to HBM
 CTCEXT_FLAG_RING_MIN = 32      # testing: the record ring at 8 frames (short items flush); implies RECORD_RING
+CTCEXT_FLAG_NO_RING = 64       # every beam record to HBM (the ring is the default for the score-table kernel)
 CTCEXT_SCORER_BASE = 0
 CTCEXT_SCORER_BIGRAM = 1
 

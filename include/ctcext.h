@@ -53,9 +53,12 @@ enum {
   CTCEXT_FLAG_PHASES = 4,          /* diagnostics: per-item s_memtime phase counters */
   CTCEXT_FLAG_GLOBAL_STATE = 8,    /* testing: decode on the global-state tier whatever the shape */
   CTCEXT_FLAG_RECORD_RING = 16,    /* keep beam records in an LDS ring and write only those the
-                                      traceback can reach (fewer HBM writes, ~1% more decode time) */
-  CTCEXT_FLAG_RING_MIN = 32        /* testing: the record ring at its smallest (8 frames), so short
+                                      traceback can reach (fewer HBM writes).  On by default
+                                      where the score-table two-wave kernel runs (float,
+                                      beam_width <= 128, num_classes <= 64); opt-in elsewhere */
+  CTCEXT_FLAG_RING_MIN = 32,       /* testing: the record ring at its smallest (8 frames), so short
                                       items flush; implies CTCEXT_FLAG_RECORD_RING */
+  CTCEXT_FLAG_NO_RING = 64         /* write every beam record to HBM (no record ring) */
 };
 
 typedef struct ctcext_decoder ctcext_decoder;

@@ -16,7 +16,7 @@ fi
 for cfg in ${CFGS:-cfg3 cfg4 cfg5}; do
   echo "== $cfg" >> $O/summary.txt
   if [ $cfg = cfg3 ]; then
-    CFG=$cfg bash tools/abv.sh ${ROUNDS:-2} "r3||ab/libr3.so|" "hw|||" "hwring|||--record-ring" "nohw|CTCEXT_HELPER=0||" >> $O/summary.txt 2>&1 || exit 1
+    CFG=$cfg bash tools/abv.sh ${ROUNDS:-2} "r3||ab/libr3.so|" "hw|||" "hwnoring|||--no-ring" "nohw|CTCEXT_HELPER=0||" >> $O/summary.txt 2>&1 || exit 1
   else
     CFG=$cfg bash tools/abv.sh ${ROUNDS:-2} "r3||ab/libr3.so|" "hw|||" "nohw|CTCEXT_HELPER=0||" >> $O/summary.txt 2>&1 || exit 1
   fi
