@@ -1740,7 +1740,7 @@ __device__ __forceinline__ void gather_chunk(const Ctx<T>& cx, int buf, int nb, 
   const T NI = ninf<T>();
   const int Cm1 = cx.C - 1;
   const int blank = cx.blank;
-  CTCX_LDS T* bmax = row_bmax(cx);
+  [[maybe_unused]] CTCX_LDS T* bmax = row_bmax(cx);
     CTCX_LDS uint64_t* cbm = row_cbm(cx);
     CTCX_LDS uint64_t* cwin = cbm + (Cm1 + 63) / 64;
     cqn = 0;
@@ -2050,7 +2050,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
   // large C: the row's maximum, its NaN / +inf test and the per 64-label block
   // maxima (bounds for window skipping in the grow loop below, in LDS after
   // the row) come from the pre-pass (ctcx_row_prep, loaded with the row)
-  CTCX_LDS T* bmax = row_bmax(cx);
+  [[maybe_unused]] CTCX_LDS T* bmax = row_bmax(cx);
   if constexpr (BIG) {   // BIG <=> C > 64
     bad |= cx.rbad != 0;
     xmax = cx.rxmax;
@@ -3542,8 +3542,8 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
   const int R = prm.ring;
   using RT = typename std::conditional<HW && !BIG, Rec32, Rec>::type;
   Ring<RT> rg{};
-  Tab tb{};
-  GQ gq{};
+  [[maybe_unused]] Tab tb{};
+  [[maybe_unused]] GQ gq{};
 #ifndef CTCX_GSTATE
   {
     size_t off = (decode_lds_bytes(WC > 0 ? WC : W, C, (int)sizeof(T), SC::kStateful) + 15) & ~(size_t)15;
