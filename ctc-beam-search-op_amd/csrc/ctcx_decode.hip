@@ -3221,6 +3221,8 @@ __host__ __device__ __attribute__((noinline)) int literal_step(Ctx<T> cx, int bu
   }
   SlotGreater<T> gt{cx.et};
   LitTop h{cx.heap, 0, W, kTopUnordered};
+  T botv = NI;        // the bottom's value, cached for the skip test below
+  bool botk = false;  // ... valid until the heap changes
 
   for (int i = 0; i < nb; ++i) {
     const int a = dup_in ? cx.alias[i] : i;
@@ -3236,8 +3238,46 @@ __host__ __device__ __attribute__((noinline)) int literal_step(Ctx<T> cx, int bu
     const int a = dup_in ? cx.alias[i] : i;
     const int bl = sel(cx.lab, buf)[i];
     const int bflg = sel(cx.flg, buf)[i];
+    // With the beam full, an offer whose child is new and scores <= bottom is
+    // rejected without effect (the reference creates the node and deactivates
+    // it; nothing reads it again), so it is scored first and dropped before
+    // the child lookup when the branch's children (up to 4 labels) do not
+    // hold its label.  bottom is peeked exactly when the reference peeks it.
+    int ch0 = -1, ch1 = -1, ch2 = -1, ch3 = -1;
+#ifdef CTCX_GSTATE
+    constexpr bool kSkip = true;
+#else
+    // (the LDS tier replays only its rare frames here: its decode kernels keep
+    // the plain loop, whose code their register allocation was tuned beside)
+    constexpr bool kSkip = false;
+#endif
+    bool skip_ok = kSkip && !dup_in;
+    if (skip_ok) {
+      int nch = 0;
+      for (int k = cx.head[a]; k >= 0; k = cx.sib[k]) {
+        const int lk = sel(cx.lab, buf)[k];
+        if (nch == 0) ch0 = lk;
+        else if (nch == 1) ch1 = lk;
+        else if (nch == 2) ch2 = lk;
+        else if (nch == 3) ch3 = lk;
+        else { skip_ok = false; break; }
+        ++nch;
+      }
+    }
+    const T b_ot = sel(cx.ot, buf)[i], b_ob = sel(cx.ob, buf)[i];
     for (int l = 0; l < C; ++l) {
       if (l == blank) continue;
+      if (skip_ok && h.size() == W && l != ch0 && l != ch1 && l != ch2 && l != ch3) {
+        T prev = (l == bl) ? b_ob : b_ot;
+        if constexpr (SC::kStateful) prev = SC::score(SC::expand(cx, sel(cx.est, buf)[i], bl, l), prev);
+        const T ct = cx.row[l] - norm + prev;
+        if (!(ct > NI)) continue;
+        if (!botk) {   // (the first peek after a change of the heap; later ones return the same)
+          botv = cx.et[lit_top_peek_bottom(h, gt)];
+          botk = true;
+        }
+        if (!(ct > botv)) continue;
+      }
       int c = -1;
       for (int k = cx.head[a]; k >= 0; k = cx.sib[k])
         if (sel(cx.lab, buf)[k] == l) { c = k; break; }
@@ -3288,6 +3328,7 @@ __host__ __device__ __attribute__((noinline)) int literal_step(Ctx<T> cx, int bu
           if (bot >= nb) cx.freel[nfree++] = bot;
         }
         lit_top_push(h, slot, gt);
+        botk = false;
       } else {
         // deactivate the child (decoder.h:200-205); a branch child's oldp and
         // old_cands are its frame-start arrays, at every position holding it
@@ -3935,16 +3976,24 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
 // T's libm (float: expf/logf; double: exp/log).  Rows past an item's length
 // are skipped.  The sums stay one thread per row (the reference's order), but
 // the row data reaches the threads through LDS: one wave owns 64 consecutive
-// rows and stages them in 64-class tiles, each tile row read as one coalesced
-// 64-lane load (HBM-bound; the first build read C strided values per thread
-// and reached ~0.2 TB/s).  Two passes over the tiles (max, then sum); for
-// C <= 64 the row stays in LDS between them.
+// rows and stages them in kNormTile-class tiles, tile rows read by coalesced
+// 64-lane loads (the first build read C strided values per thread and
+// reached ~0.2 TB/s).  Two passes over the tiles (max, then sum; for C > 64
+// the max comes from ctcx_row_facts' header); for C <= kNormTile the row
+// stays in LDS between them.
 __host__ __device__ __forceinline__ float norm_exp(float x) { return gm::expf(x); }
 __host__ __device__ __forceinline__ double norm_exp(double x) { return gm::exp(x); }
 __host__ __device__ __forceinline__ float norm_log(float x) { return gm::logf(x); }
 __host__ __device__ __forceinline__ double norm_log(double x) { return gm::log(x); }
 
-constexpr int kNormTile = 64;
+#ifndef CTCX_NORM_TILE
+#define CTCX_NORM_TILE 32
+#endif
+// classes per tile: 32 (two rows per 64-lane load) keeps a wave's tile at 8.4
+// KB of LDS (float), so LDS no longer caps the kernel at ~2 waves per SIMD
+constexpr int kNormTile = CTCX_NORM_TILE;
+constexpr int kNormRPL = 64 / kNormTile;   // tile rows per load instruction
+constexpr int kNormNL = 64 / kNormRPL;     // load instructions per tile
 
 template <typename T>
 __global__ __launch_bounds__(64) void ctcx_row_norm(const T* __restrict__ x, const int32_t* seq_len,
@@ -3976,22 +4025,34 @@ __global__ __launch_bounds__(64) void ctcx_row_norm(const T* __restrict__ x, con
     if (!h.bad) { m = h.xmax; known = true; }
   }
   const bool pass0 = __ballot(valid && !known) != 0ull;
-  auto load = [&](T (&v)[64], int64_t c0) {
-    // row rr of the tile: one load per lane, sizeof(T) * nc contiguous bytes
-    // (an invalid row reads x's first row instead and is never used)
+  const int sub = lane / kNormTile, col = lane % kNormTile;   // a load's tile row (of kNormRPL) and class
+  auto row_base = [&](int rr) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)off, rr);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)off >> 32), rr);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+  };
+  auto load = [&](T (&v)[kNormNL], int64_t c0) {
+    // tile rows q * kNormRPL + sub: one load per lane, sizeof(T) * nc
+    // contiguous bytes per row (an invalid row reads x's first row instead
+    // and is never used)
     const int nc = (int)(C - c0 < kNormTile ? C - c0 : kNormTile);
-    const int col = lane < nc ? (int)c0 + lane : 0;
+    const int cc = col < nc ? (int)c0 + col : 0;
 #pragma unroll
-    for (int rr = 0; rr < 64; ++rr) {
-      const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)off, rr);
-      const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)off >> 32), rr);
-      v[rr] = x[(int64_t)(((uint64_t)hi << 32) | lo) + col];
+    for (int q = 0; q < kNormNL; ++q) {
+      int64_t base;
+      if constexpr (kNormRPL == 1) {
+        base = row_base(q);
+      } else {
+        const int64_t b0 = row_base(2 * q), b1 = row_base(2 * q + 1);
+        base = sub ? b1 : b0;
+      }
+      v[q] = x[base + cc];
     }
   };
-  T v[64];
+  T v[kNormNL];
   for (int pass = pass0 ? 0 : 1; pass < 2; ++pass) {
-    // the tile is (re)loaded unless C <= 64 and pass 0 left it in LDS; the
-    // next tile's loads are issued before this tile's sums (software pipeline)
+    // the tile is (re)loaded unless C <= kNormTile and pass 0 left it in LDS;
+    // the next tile's loads are issued before this tile's sums (software pipeline)
     const bool reload = pass == 0 || C > kNormTile || !pass0;
     if (reload) load(v, 0);
     for (int64_t c0 = 0; c0 < C; c0 += kNormTile) {
@@ -3999,7 +4060,7 @@ __global__ __launch_bounds__(64) void ctcx_row_norm(const T* __restrict__ x, con
       if (reload) {
         __syncthreads();
 #pragma unroll
-        for (int rr = 0; rr < 64; ++rr) tile[rr][lane] = v[rr];
+        for (int q = 0; q < kNormNL; ++q) tile[q * kNormRPL + sub][col] = v[q];
         __syncthreads();
         if (c0 + kNormTile < C) load(v, c0 + kNormTile);
       }
@@ -4011,7 +4072,20 @@ __global__ __launch_bounds__(64) void ctcx_row_norm(const T* __restrict__ x, con
             for (; j < nc; ++j) { const T e = tile[lane][j]; m = (e > m) ? e : m; }
           }
         } else if constexpr (sizeof(T) == 4) {
-          for (int j = 0; j < nc; ++j) s += gm::expf_t(tile[lane][j] - m, etab);
+          if (nc == kNormTile) {
+            // a whole tile: the exp terms are independent (computed 16 at a
+            // time, in flight together), only the sum is a chain, in class order
+#pragma unroll
+            for (int j0 = 0; j0 < kNormTile; j0 += 16) {
+              T e[16];
+#pragma unroll
+              for (int j = 0; j < 16; ++j) e[j] = gm::expf_t(tile[lane][j0 + j] - m, etab);
+#pragma unroll
+              for (int j = 0; j < 16; ++j) s += e[j];
+            }
+          } else {
+            for (int j = 0; j < nc; ++j) s += gm::expf_t(tile[lane][j] - m, etab);
+          }
         } else {
           for (int j = 0; j < nc; ++j) s += norm_exp(tile[lane][j] - m);
         }
@@ -4265,14 +4339,80 @@ __global__ __launch_bounds__(64) void ctcx_row_prep(const T* __restrict__ x, con
 // header written here): the one-lane class-order sum of ctcx_row_prep was the
 // bulk of its time.  Four rows per 256-thread block, one per wave.
 // keys at or above the first bracket's lower end (the smallest lane maximum)
-// kept for the in-register bisection: at C = 5000, N(0,1) rows hold ~270 of
-// them, past ctcx_row_prep's 256 (whose fallback bisects over all C keys)
+// kept for the radix select: at C = 5000, N(0,1) rows hold ~270 of them,
+// past ctcx_row_prep's 256 (whose fallback bisects over all C keys)
+#ifndef CTCX_FACTS_WPE
+#define CTCX_FACTS_WPE 1
+#endif
 constexpr int kFactsCompact = 1024;
+// The (rank)-th largest of the n keys of a wave's compact list (rank <= n):
+// MSB-first radix select, 8-bit digits, a 256-bin LDS histogram per pass.
+// Every key lies in [klo, khi], so the bits above their highest differing bit
+// are common and skipped (three passes for the N(0,1) rows at C = 5000).
+__device__ __forceinline__ unsigned radix_select_desc(const unsigned* cks, int n, int rank, unsigned klo,
+                                                      unsigned khi, unsigned* hist) {
+  const int lane = threadIdx.x & 63;
+  const unsigned diff = klo ^ khi;
+  if (diff == 0u) return klo;
+  int rem = 32 - __builtin_clz(diff);   // bits below the common prefix
+  unsigned pfx = rem == 32 ? 0u : (klo >> rem) << rem;
+  const int nq = (n + 63) >> 6;
+  auto wsync_lds = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  while (rem > 0) {
+    const int wd = rem < 8 ? rem : 8;
+    const int sh = rem - wd;
+    ((uint4*)hist)[lane] = make_uint4(0u, 0u, 0u, 0u);
+    wsync_lds();
+    for (int q = 0; q < nq; ++q) {
+      const int j = 64 * q + lane;
+      const unsigned kv = cks[j < n ? j : 0];
+      // the key matches the digits chosen so far: its bits at and above sh + wd equal pfx's
+      const bool match = j < n && (((uint64_t)(kv ^ pfx) >> (sh + wd)) == 0ull);
+      if (match)
+        __hip_atomic_fetch_add(&hist[(kv >> sh) & ((1u << wd) - 1u)], 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    wsync_lds();
+    const uint4 hb = ((const uint4*)hist)[lane];   // bins 4 lane .. 4 lane + 3
+    const int tl = (int)(hb.x + hb.y + hb.z + hb.w);
+    // inclusive suffix sum over lanes: the keys in bins >= 4 lane
+    int sfx = tl;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int o = __shfl_down(sfx, d);
+      sfx += lane + d < 64 ? o : 0;
+    }
+    const int above = sfx - tl;   // keys in the bins of the lanes above
+    const uint64_t hit = __ballot(above < rank && rank <= sfx);
+    const int L = __builtin_ctzll(hit);
+    int dg, ab;   // the digit, the keys in the bins above it
+    if (above + (int)hb.w >= rank) { dg = 3; ab = above; }
+    else if (above + (int)(hb.w + hb.z) >= rank) { dg = 2; ab = above + (int)hb.w; }
+    else if (above + (int)(hb.w + hb.z + hb.y) >= rank) { dg = 1; ab = above + (int)(hb.w + hb.z); }
+    else { dg = 0; ab = above + (int)(hb.w + hb.z + hb.y); }
+    dg = __builtin_amdgcn_readlane(4 * lane + dg, L);
+    ab = __builtin_amdgcn_readlane(ab, L);
+    rank -= ab;
+    pfx |= (unsigned)dg << sh;
+    rem = sh;
+    wsync_lds();   // the histogram is cleared again only after every lane has read it
+  }
+  return pfx;
+}
+
 template <int NV>
-__global__ __launch_bounds__(256) void ctcx_row_facts(const float* __restrict__ x,
-                                                     const int32_t* __restrict__ seq_len, char* __restrict__ prep,
-                                                     int64_t rows, int64_t B, int C, int64_t xstride, int blank) {
-  __shared__ unsigned cks_all[4][kFactsCompact];
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_WPE, 8))) void ctcx_row_facts(
+    const float* __restrict__ x, const int32_t* __restrict__ seq_len, char* __restrict__ prep, int64_t rows,
+    int64_t B, int C, int64_t xstride, int blank) {
+  // per wave: the compact list of (key, label index) in label order, with one
+  // dummy slot per lane (its stores are unconditional), and the radix histogram
+  __shared__ unsigned cks_all[4][kFactsCompact + 64];
+  __shared__ unsigned cls_all[4][kFactsCompact + 64];
+  __shared__ unsigned hist_all[4][256];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t row = (int64_t)blockIdx.x * 4 + wv;
   if (row >= rows) return;   // wave-uniform, and no block barrier below
@@ -4283,6 +4423,7 @@ __global__ __launch_bounds__(256) void ctcx_row_facts(const float* __restrict__ 
   const float4* xr = (const float4*)(x + (t * xstride + b) * (int64_t)C);
   char* pr = prep + row * (int64_t)prep_row_bytes(C, 4);
   float* bm = (float*)(pr + prep_bmax_offset(4));
+  uint2* top = (uint2*)(pr + prep_top_offset(C, 4));
   const int nblk = (C + 63) / 64;
   // the row, then its keys: fkey of each non-blank class, 0 for the blank and
   // the padding (fkey is order-preserving; 0 is the key of one NaN pattern
@@ -4297,9 +4438,11 @@ __global__ __launch_bounds__(256) void ctcx_row_facts(const float* __restrict__ 
     k[u][2] = __float_as_uint(f.z); k[u][3] = __float_as_uint(f.w);
   }
   // maximum, NaN / +inf, the block maxima (block 4 u + (lane >> 4) is the
-  // 16-lane DPP row of one u: its maximum lands on the row's lane 15)
+  // 16-lane DPP row of one u: its maximum lands on the row's lane 15), and
+  // the lane's largest key
   float xmax = NI;
   bool bad = false;
+  unsigned lk = 0u;
 #pragma unroll
   for (int u = 0; u < NV; ++u) {
     float lm = NI;
@@ -4310,6 +4453,7 @@ __global__ __launch_bounds__(256) void ctcx_row_facts(const float* __restrict__ 
       lm = v > lm ? v : lm;
       const int cl = 4 * (64 * u + lane) + c;
       k[u][c] = (64 * u + lane < C4 && cl != blank) ? fkey(v) : 0u;
+      lk = k[u][c] > lk ? k[u][c] : lk;
     }
     xmax = lm > xmax ? lm : xmax;
     float w;
@@ -4323,113 +4467,130 @@ __global__ __launch_bounds__(256) void ctcx_row_facts(const float* __restrict__ 
   RowHdr<float> h;
   h.xmax = wave_max_dpp(xmax);
   h.bad = __ballot(bad) != 0ull;
+#ifdef CTCX_FACTS_LOADONLY   // timing experiments only: the row's load and first pass
+  h.ns = 0;
+  h.xout = __uint_as_float(lk);
+  if (lane == 0) *(RowHdr<float>*)pr = h;
+  return;
+#endif
   const int K = kTopK;
-  // |{non-blank classes with key >= tau}| for tau >= 1
-  auto cnt_ge = [&](unsigned tau) __attribute__((always_inline)) {
-    int n = 0;
-#pragma unroll
-    for (int u = 0; u < NV; ++u)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) n += k[u][c] >= tau ? 1 : 0;
-    return uni(wave_sum_dpp(n));
-  };
-  auto bisect = [&](uint64_t& lo, uint64_t& hi) __attribute__((always_inline)) {
-    while (hi - lo > 1) {
-      const uint64_t mid = (lo + hi) >> 1;
-      const int c = cnt_ge((unsigned)mid);
-      if (c <= K) hi = mid;
-      else lo = mid;
-      if (c == K) break;
-    }
-  };
-  uint64_t lo = 0, hi = 1;   // tau in (lo, hi]: cnt(lo) > K >= cnt(hi); C - 1 <= K: tau = 1, all of them
-  if (C - 1 > K) {
-    hi = (uint64_t)fkey(h.xmax) + 1ull;   // cnt(hi) = 0
-    // the smallest lane maximum km: one key per lane at or above it, so
-    // cnt(km) >= 64 when every lane holds a label (C >= 256; else km = 0)
-    unsigned lk = 0u;
-#pragma unroll
-    for (int u = 0; u < NV; ++u)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) lk = k[u][c] > lk ? k[u][c] : lk;
-    const unsigned km = (unsigned)uni((int)wave_min_dpp(lk));
-    const int ckm = km > 0u ? cnt_ge(km) : C - 1;
-    if (km > 0u && ckm == K) {
-      lo = km - 1;   // exactly the K largest: tau = km
-      hi = km;
-    } else if (km > 0u && ckm <= kFactsCompact) {
-      // every key >= km into a compact list, then bisect in registers
-      lo = km;
-      unsigned* cks = cks_all[wv];
-      int n = 0;
-#pragma unroll
-      for (int u = 0; u < NV; ++u)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const bool in = k[u][c] >= km;
-          const uint64_t mm = __ballot(in);
-          if (in) cks[n + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mm >> 32),
-                                                         __builtin_amdgcn_mbcnt_lo((unsigned)mm, 0u))] = k[u][c];
-          n += __builtin_popcountll(mm);
-        }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      unsigned ck[kFactsCompact / 64];
-#pragma unroll
-      for (int q = 0; q < kFactsCompact / 64; ++q) ck[q] = 64 * q + lane < n ? cks[64 * q + lane] : 0u;
-      while (hi - lo > 1) {
-        const uint64_t mid = (lo + hi) >> 1;
-        int c = 0;
-#pragma unroll
-        for (int q = 0; q < kFactsCompact / 64; ++q) c += ck[q] >= (unsigned)mid ? 1 : 0;
-        c = uni(wave_sum_dpp(c));
-        if (c <= K) hi = mid;
-        else lo = mid;
-        if (c == K) break;
-      }
-    } else {
-      if (km > 0u) lo = km;   // cnt(km) > K; else cnt(0) = C - 1 > K
-      bisect(lo, hi);
-    }
-  }
-  // S in label-index order (within a u, class order is (lane, c) order), and
-  // the largest key of a label outside it
-  const unsigned tau = (unsigned)hi;
-  uint2* top = (uint2*)(pr + prep_top_offset(C, 4));
-  unsigned ko = 0u;
-  int n = 0;
+  auto unkey = [](unsigned kv) { return kv ^ ((kv >> 31) ? 0x80000000u : 0xFFFFFFFFu); };   // fkey's inverse
   const uint64_t ltm = (1ull << lane) - 1ull;
+  // S = the keys >= tau, tau the smallest threshold with |S| <= K: one past
+  // the (K+1)-th largest key v, and the largest key outside S is then v
+  // itself (C - 1 <= K: every label, nothing outside).  The smallest lane
+  // maximum km bounds v from below: one key per lane at or above it (when
+  // every lane holds a label, C >= 256; else km = 0 and the bound is 1).
+  const unsigned km = (unsigned)uni((int)wave_min_dpp(lk));
+  const unsigned kmx = (unsigned)uni((int)~wave_min_dpp(~lk));   // the largest key
+  const unsigned kt = km > 1u ? km : 1u;
+  // every key >= kt into the compact list, in label order (within a u, label
+  // order is (lane, c) order): a label's slot is the count before it
+  unsigned* cks = cks_all[wv];
+  unsigned* cls = cls_all[wv];
+  int n = 0;
 #pragma unroll
   for (int u = 0; u < NV; ++u) {
     if (64 * u < C4) {   // uniform
       bool in[4];
-      uint64_t mm[4];
       int before = 0;
+      uint64_t mm[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        in[c] = k[u][c] >= tau;
-        if (!in[c]) ko = k[u][c] > ko ? k[u][c] : ko;
+        in[c] = k[u][c] >= kt;
         mm[c] = __ballot(in[c]);
-        before += __builtin_popcountll(mm[c] & ltm);
+        before += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mm[c] >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mm[c], 0u));
       }
+      int at = n + before;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        if (in[c]) {
-          const int cl = 4 * (64 * u + lane) + c;
-          const unsigned kv = k[u][c];
-          const unsigned bits = kv ^ ((kv >> 31) ? 0x80000000u : 0xFFFFFFFFu);   // fkey's inverse
-          top[n + before] = make_uint2(bits, (unsigned)(cl - (cl > blank ? 1 : 0)));
-          ++before;
-        }
+        const int cl = 4 * (64 * u + lane) + c;
+        const int j = (in[c] && at < kFactsCompact) ? at : kFactsCompact + lane;
+        cks[j] = k[u][c];
+        cls[j] = (unsigned)(cl - (cl > blank ? 1 : 0));
+        at += in[c] ? 1 : 0;
       }
 #pragma unroll
       for (int c = 0; c < 4; ++c) n += __builtin_popcountll(mm[c]);
     }
   }
-  h.ns = n;
-  ko = (unsigned)uni((int)~wave_min_dpp(~ko));   // the wave's largest
-  h.xout = ko == 0u ? NI : __uint_as_float(ko ^ ((ko >> 31) ? 0x80000000u : 0xFFFFFFFFu));
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (n <= kFactsCompact && (n > K || C - 1 <= K)) {
+    // S from the list: all of it (C - 1 <= K), or the keys above the
+    // (K+1)-th largest, found by a radix select over the list
+    unsigned v = 0u;
+    if (C - 1 > K) v = radix_select_desc(cks, n, K + 1, kt, kmx, hist_all[wv]);
+    int ns = 0;
+    for (int j0 = 0; j0 < n; j0 += 64) {
+      const int j = j0 + lane;
+      const unsigned kv = j < n ? cks[j] : 0u;
+      const bool in = j < n && kv > v;
+      const uint64_t mm = __ballot(in);
+      if (in) {
+        const int r = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mm, 0u));
+        top[ns + r] = make_uint2(unkey(kv), cls[j]);
+      }
+      ns += __builtin_popcountll(mm);
+    }
+    h.ns = ns;
+    h.xout = v == 0u ? NI : __uint_as_float(unkey(v));
+  } else {
+    // the rare shapes: exactly K keys at or above km (S is the list, its
+    // outside maximum taken from the registers), or a list past its capacity
+    // (tau bisected over the row's keys, S from the registers)
+    auto cnt_ge = [&](unsigned tau) __attribute__((always_inline)) {
+      int c2 = 0;
+#pragma unroll
+      for (int u = 0; u < NV; ++u)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) c2 += k[u][c] >= tau ? 1 : 0;
+      return uni(wave_sum_dpp(c2));
+    };
+    unsigned tau = kt;
+    if (n > K) {
+      uint64_t lo = kt - 1u, hi = (uint64_t)kmx + 1ull;   // cnt(lo) >= cnt(kt) > K >= cnt(hi) = 0
+      while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) >> 1;
+        const int c2 = cnt_ge((unsigned)mid);
+        if (c2 <= K) hi = mid;
+        else lo = mid;
+        if (c2 == K) break;
+      }
+      tau = (unsigned)hi;
+    }
+    unsigned ko = 0u;
+    int ns = 0;
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      if (64 * u < C4) {   // uniform
+        bool in[4];
+        uint64_t mm[4];
+        int before = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          in[c] = k[u][c] >= tau;
+          if (!in[c]) ko = k[u][c] > ko ? k[u][c] : ko;
+          mm[c] = __ballot(in[c]);
+          before += __builtin_popcountll(mm[c] & ltm);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (in[c]) {
+            const int cl = 4 * (64 * u + lane) + c;
+            top[ns + before] = make_uint2(unkey(k[u][c]), (unsigned)(cl - (cl > blank ? 1 : 0)));
+            ++before;
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) ns += __builtin_popcountll(mm[c]);
+      }
+    }
+    h.ns = ns;
+    ko = (unsigned)uni((int)~wave_min_dpp(~ko));   // the wave's largest
+    h.xout = ko == 0u ? NI : __uint_as_float(unkey(ko));
+  }
   if (lane == 0) *(RowHdr<float>*)pr = h;
 }
 
