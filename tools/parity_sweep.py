@@ -34,6 +34,10 @@ FAMILIES = {
     # global-state tier forced onto small mixed cases
     "large_c_2k": (5012, dict(T_max=14, B_max=2, C_min=2049, C_max=3000, W_min=32, W_max=256)),
     "gstate_mixed": (5013, dict(T_max=30, B_max=2, C_max=80, W_max=60, flags="gstate")),
+    # round 4: the global-state tier's early rejection of new children (beam
+    # full, larger C, ties deciding the bottom)
+    "gstate_large_c": (5014, dict(T_max=15, B_max=2, C_min=65, C_max=600, W_min=4, W_max=64, flags="gstate")),
+    "gstate_ties": (5015, dict(T_max=20, B_max=2, C_max=40, W_max=48, ties=True, flags="gstate")),
 }
 total = 0
 t0 = time.time()
