@@ -3197,6 +3197,237 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
 // Positions holding the same entry are linked by cx.alias (the first
 // occurrence, which owns the entry slot); dup_in says this frame has any, and
 // *dup_out that the next one does.
+#ifdef CTCX_GSTATE
+template <typename T, class SC, bool WAVE = true>
+__host__ __device__ __attribute__((noinline)) int literal_step(Ctx<T> cx, int buf, int nb, T norm, bool last, int P,
+                                                               bool dup_in, int* dup_out, int* n_leaves) {
+  const T NI = ninf<T>();
+  const int W = cx.W, C = cx.C, blank = cx.blank;
+  // WAVE (the global-state tier): the whole wave enters; lane 0 alone runs
+  // the replay and owns every state write, the other lanes only help scan a
+  // branch's offers (below).  Otherwise one lane runs it all.
+#ifdef __HIP_DEVICE_COMPILE__
+  const bool me = !WAVE || (threadIdx.x & 63) == 0;
+#else
+  const bool me = true;
+#endif
+  int nfree = 0;
+  SlotGreater<T> gt{cx.et};
+  LitTop h{cx.heap, 0, W, kTopUnordered};
+  if (me) {
+    // roll (decoder.h:87-92)
+    for (int i = 0; i < nb; ++i) {
+      const int a = dup_in ? cx.alias[i] : i;
+      if (a == i) {
+        cx.et[i] = sel(cx.ot, buf)[i]; cx.eb[i] = sel(cx.ob, buf)[i]; cx.el[i] = sel(cx.ol, buf)[i];
+        cx.eflg[i] = 0;
+        cx.bst[i] = 0;
+      } else {   // a second roll of the entry: old_cands = (reset) new_cands
+        sel(cx.flg, buf)[i] &= ~(F_HB | F_HN);
+        sel(cx.flg, buf)[a] &= ~(F_HB | F_HN);
+      }
+    }
+    for (int s = cx.enc - 1; s >= nb; --s) {
+      cx.freel[nfree++] = s;
+      if (dup_in) cx.ekind[s] = 0xFFFFFFFFu;   // no stale match in the child lookup below
+    }
+    for (int i = 0; i < nb; ++i) {
+      const int a = dup_in ? cx.alias[i] : i;
+      recurse_branch<T, SC>(cx, buf, i, a, norm, true);
+      lit_top_push(h, a, gt);
+    }
+  }
+  // WAVE: lane 0's heap facts for the scan -- full, and the bottom's value
+  // once the heap has been peeked since its last change (botk)
+  [[maybe_unused]] auto heap_facts = [&](int& full, int& botk, T& botv) {
+    full = (me && h.size() == W) ? 1 : 0;
+    botk = (me && full && h.state != kTopUnordered) ? 1 : 0;
+    botv = botk ? cx.et[h.e[0]] : NI;
+    if constexpr (WAVE) {
+#ifdef __HIP_DEVICE_COMPILE__
+      full = __builtin_amdgcn_readfirstlane(full);
+      botk = __builtin_amdgcn_readfirstlane(botk);
+      botv = bcast(botv, 0);
+#endif
+    }
+  };
+
+  for (int i = 0; i < nb; ++i) {
+    int go = 0;
+    if (me) {
+      const T bt = sel(cx.ot, buf)[i];
+      go = (bt > NI && (h.size() < W || bt > cx.et[lit_top_peek_bottom(h, gt)])) ? 1 : 0;
+    }
+#ifdef __HIP_DEVICE_COMPILE__
+    if constexpr (WAVE) go = __builtin_amdgcn_readfirstlane(go);
+#endif
+    if (!go) continue;
+    const int a = dup_in ? cx.alias[i] : i;
+    const int bl = sel(cx.lab, buf)[i];
+    const int bflg = sel(cx.flg, buf)[i];
+    // One offer (decoder.h:160-208), lane 0.
+    auto offer = [&](int l) {
+      int c = -1;
+      for (int k = cx.head[a]; k >= 0; k = cx.sib[k])
+        if (sel(cx.lab, buf)[k] == l) { c = k; break; }
+      if (c < 0 && dup_in) {
+        // GetChild of an entry visited twice: the child an earlier visit created
+        // this frame is the same node (Active: skipped; otherwise re-created)
+        bool act = false;
+        for (int s = nb; s < cx.enc; ++s)
+          if (cx.ekind[s] == (((uint32_t)a << 1) | 1u) && cx.elab[s] == l && cx.et[s] != NI) { act = true; break; }
+        if (act) return;
+      }
+      int slot;
+      const bool fresh_slot = (c < 0);
+      if (!fresh_slot) {
+        slot = c;
+        if (cx.et[c] != NI) return;            // c.Active()
+      } else {
+        slot = cx.freel[nfree - 1];
+        cx.eflg[slot] = 0;
+      }
+      const T xl = cx.row[l];
+      const T p = xl - norm;
+      cx.eb[slot] = NI;
+      T prev = (l == bl) ? sel(cx.ob, buf)[i] : sel(cx.ot, buf)[i];
+      if constexpr (SC::kStateful) {
+        const T cst = SC::expand(cx, sel(cx.est, buf)[i], bl, l);   // ExpandState (decoder.h:171)
+        cx.eest[slot] = cst;
+        prev = SC::score(cst, prev);
+      }
+      cx.el[slot] = xl - norm + prev;
+      const bool recv_fresh = fresh_slot ? true : (sel(cx.ot, buf)[c] == NI);
+      const T rs_blank = ((bflg & F_ROOT) && recv_fresh) ? T(0) : NI;
+      Best<T> cd{cx.ecn[slot], cx.ebpn[slot], (cx.eflg[slot] & F_HN) != 0};
+      cand_from(cx, buf, i, 0, p, rs_blank, cd);
+      if (l != bl) cand_from(cx, buf, i, 1, p, NI, cd);
+      cx.ecn[slot] = cd.p; cx.ebpn[slot] = cd.bp;
+      cx.eflg[slot] |= F_HN;
+      cx.et[slot] = cx.el[slot];
+      cx.ekind[slot] = fresh_slot ? (((uint32_t)a << 1) | 1u) : ((uint32_t)c << 1);
+      cx.elab[slot] = l;
+      const T ct = cx.et[slot];
+      if (ct > NI && (h.size() < W || ct > cx.et[lit_top_peek_bottom(h, gt)])) {
+        if (fresh_slot) nfree--;
+        if (h.size() == W) {
+          const int bot = lit_top_peek_bottom(h, gt);
+          cx.et[bot] = NI; cx.eb[bot] = NI; cx.el[bot] = NI;
+          cx.eflg[bot] = 0;
+          if (bot >= nb) cx.freel[nfree++] = bot;
+        }
+        lit_top_push(h, slot, gt);
+      } else {
+        // deactivate the child (decoder.h:200-205); a branch child's oldp and
+        // old_cands are its frame-start arrays, at every position holding it
+        cx.et[slot] = NI; cx.eb[slot] = NI; cx.el[slot] = NI;
+        cx.eflg[slot] = 0;
+        if (!fresh_slot) {
+          for (int j = c; j < nb; ++j) {
+            if (j != c && !(dup_in && cx.alias[j] == c)) continue;
+            sel(cx.ot, buf)[j] = NI; sel(cx.ob, buf)[j] = NI; sel(cx.ol, buf)[j] = NI;
+            sel(cx.flg, buf)[j] &= ~(F_HB | F_HN);
+            if (!dup_in) break;
+          }
+        }
+      }
+    };
+    if constexpr (!WAVE) {
+      for (int l = 0; l < C; ++l)
+        if (l != blank) offer(l);
+    } else {
+#ifdef __HIP_DEVICE_COMPILE__
+      // With the beam full, an offer whose child is new and scores <= bottom is
+      // rejected without effect (the reference creates the node and deactivates
+      // it; nothing reads it again).  So the wave scores 64 labels at a time
+      // and lane 0 replays only the offers that can matter: a label of one of
+      // the branch's children (up to 4 kept; more: no scan), or a new child
+      // scoring above the bottom -- any score above -inf while the bottom is
+      // not known, since the reference's peek happens at that offer (lane 0
+      // does it there).  The bottom only rises, so the scan's bottom, from
+      // before the offers it lets through, passes a superset.
+      const int lane = threadIdx.x & 63;
+      int ch0 = -1, ch1 = -1, ch2 = -1, ch3 = -1;
+      bool scan = !dup_in;
+      if (scan) {
+        int nch = 0;
+        for (int k = cx.head[a]; k >= 0; k = cx.sib[k]) {
+          const int lk = sel(cx.lab, buf)[k];
+          if (nch == 0) ch0 = lk;
+          else if (nch == 1) ch1 = lk;
+          else if (nch == 2) ch2 = lk;
+          else if (nch == 3) ch3 = lk;
+          else { scan = false; break; }
+          ++nch;
+        }
+      }
+      const T b_ot = sel(cx.ot, buf)[i], b_ob = sel(cx.ob, buf)[i];
+      int full, botk;
+      T botv;
+      heap_facts(full, botk, botv);
+      for (int l = 0; l < C;) {
+        if (scan && full) {
+          uint64_t want = 0ull;
+          for (; l < C; l += 64) {
+            const int lq = l + lane;
+            bool w = false;
+            if (lq < C && lq != blank) {
+              if (lq == ch0 || lq == ch1 || lq == ch2 || lq == ch3) {
+                w = true;
+              } else {
+                T prev = (lq == bl) ? b_ob : b_ot;
+                if constexpr (SC::kStateful) prev = SC::score(SC::expand(cx, sel(cx.est, buf)[i], bl, lq), prev);
+                const T ct = cx.row[lq] - norm + prev;
+                w = ct > NI && (!botk || ct > botv);
+              }
+            }
+            want = __ballot(w);
+            if (want) break;
+          }
+          if (l >= C) break;
+          l += __builtin_ctzll(want);
+        } else if (l == blank) {
+          ++l;
+          continue;
+        }
+        if (me) offer(l);
+        ++l;
+        heap_facts(full, botk, botv);
+      }
+#endif
+    }
+  }
+  if (!me) return 0;   // (WAVE: lane 0's count is the result)
+  *n_leaves = h.size();
+  if (last) {
+    const int lim = P < W ? P : W;
+    LitTop tp{cx.tops, 0, lim, kTopUnordered};
+    for (int q = 0; q < h.size(); ++q) lit_top_push(tp, h.e[q], gt);
+    lit_top_extract(tp, gt);
+  }
+  const int n = lit_top_extract(h, gt);
+  // slot -> first sorted position (freel reused as the map; -1 = not a leaf);
+  // the next frame's aliases
+  for (int s = 0; s < cx.enc; ++s) cx.freel[s] = -1;
+  int dup = 0;
+  for (int k = 0; k < n; ++k) {
+    const int s = cx.heap[k];
+    if (cx.freel[s] < 0) cx.freel[s] = k;
+    else dup = 1;
+    cx.sorted[k] = s;
+    cx.alias[k] = cx.freel[s];
+  }
+  *dup_out = dup;
+  if (last) {
+    const int lim = (P < *n_leaves) ? P : *n_leaves;
+    for (int q = 0; q < lim; ++q) cx.tops[q] = cx.freel[cx.tops[q]];
+  }
+  return n;
+}
+
+#else
+// (the LDS tier's copy: one lane, every offer; it replays only the rare
+// frames, and its decode kernels' register allocation was tuned beside it)
 template <typename T, class SC>
 __host__ __device__ __attribute__((noinline)) int literal_step(Ctx<T> cx, int buf, int nb, T norm, bool last, int P,
                                                                bool dup_in, int* dup_out, int* n_leaves) {
@@ -3221,8 +3452,6 @@ __host__ __device__ __attribute__((noinline)) int literal_step(Ctx<T> cx, int bu
   }
   SlotGreater<T> gt{cx.et};
   LitTop h{cx.heap, 0, W, kTopUnordered};
-  T botv = NI;        // the bottom's value, cached for the skip test below
-  bool botk = false;  // ... valid until the heap changes
 
   for (int i = 0; i < nb; ++i) {
     const int a = dup_in ? cx.alias[i] : i;
@@ -3238,46 +3467,8 @@ __host__ __device__ __attribute__((noinline)) int literal_step(Ctx<T> cx, int bu
     const int a = dup_in ? cx.alias[i] : i;
     const int bl = sel(cx.lab, buf)[i];
     const int bflg = sel(cx.flg, buf)[i];
-    // With the beam full, an offer whose child is new and scores <= bottom is
-    // rejected without effect (the reference creates the node and deactivates
-    // it; nothing reads it again), so it is scored first and dropped before
-    // the child lookup when the branch's children (up to 4 labels) do not
-    // hold its label.  bottom is peeked exactly when the reference peeks it.
-    int ch0 = -1, ch1 = -1, ch2 = -1, ch3 = -1;
-#ifdef CTCX_GSTATE
-    constexpr bool kSkip = true;
-#else
-    // (the LDS tier replays only its rare frames here: its decode kernels keep
-    // the plain loop, whose code their register allocation was tuned beside)
-    constexpr bool kSkip = false;
-#endif
-    bool skip_ok = kSkip && !dup_in;
-    if (skip_ok) {
-      int nch = 0;
-      for (int k = cx.head[a]; k >= 0; k = cx.sib[k]) {
-        const int lk = sel(cx.lab, buf)[k];
-        if (nch == 0) ch0 = lk;
-        else if (nch == 1) ch1 = lk;
-        else if (nch == 2) ch2 = lk;
-        else if (nch == 3) ch3 = lk;
-        else { skip_ok = false; break; }
-        ++nch;
-      }
-    }
-    const T b_ot = sel(cx.ot, buf)[i], b_ob = sel(cx.ob, buf)[i];
     for (int l = 0; l < C; ++l) {
       if (l == blank) continue;
-      if (skip_ok && h.size() == W && l != ch0 && l != ch1 && l != ch2 && l != ch3) {
-        T prev = (l == bl) ? b_ob : b_ot;
-        if constexpr (SC::kStateful) prev = SC::score(SC::expand(cx, sel(cx.est, buf)[i], bl, l), prev);
-        const T ct = cx.row[l] - norm + prev;
-        if (!(ct > NI)) continue;
-        if (!botk) {   // (the first peek after a change of the heap; later ones return the same)
-          botv = cx.et[lit_top_peek_bottom(h, gt)];
-          botk = true;
-        }
-        if (!(ct > botv)) continue;
-      }
       int c = -1;
       for (int k = cx.head[a]; k >= 0; k = cx.sib[k])
         if (sel(cx.lab, buf)[k] == l) { c = k; break; }
@@ -3328,7 +3519,6 @@ __host__ __device__ __attribute__((noinline)) int literal_step(Ctx<T> cx, int bu
           if (bot >= nb) cx.freel[nfree++] = bot;
         }
         lit_top_push(h, slot, gt);
-        botk = false;
       } else {
         // deactivate the child (decoder.h:200-205); a branch child's oldp and
         // old_cands are its frame-start arrays, at every position holding it
@@ -3372,6 +3562,8 @@ __host__ __device__ __attribute__((noinline)) int literal_step(Ctx<T> cx, int bu
   }
   return n;
 }
+
+#endif
 
 // ---------------------------------------------------------------------------
 // Record ring (LDS tier).  The traceback reads back only the P final paths'
@@ -3736,12 +3928,25 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
     dup_frames += dup ? 1 : 0;
     bool dup_next = false;
     if (!ok) {
+#ifdef CTCX_GSTATE
+      // every frame is replayed here: wave 0 scans the offers with lane 0
+      if (tid < 64) {
+        int d2 = 0, nl = 0;
+        const int nn = literal_step<T, SC, true>(cx, buf, nb, norm, last, prm.P, dup, &d2, &nl);
+        if (tid == 0) {
+          misc[0] = nn;
+          misc[1] = d2;
+          misc[2] = nl;
+        }
+      }
+#else
       if (tid == 0) {
         int d2 = 0, nl = 0;
         misc[0] = literal_step<T, SC>(cx, buf, nb, norm, last, prm.P, dup, &d2, &nl);
         misc[1] = d2;
         misc[2] = nl;
       }
+#endif
       __syncthreads();
       n = misc[0];
       dup_next = uni(misc[1]) != 0;   // wave-uniform: the next frame's exact_step call stays uniform
@@ -4429,13 +4634,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_
   // the padding (fkey is order-preserving; 0 is the key of one NaN pattern
   // only, and a row holding a NaN is decoded literally, without S)
   unsigned k[NV][4];
+  // buffer loads: one lane offset and a constant row offset per load, no
+  // 64-bit address per load in flight (those took 40 VGPRs at NV = 20); past
+  // the row they return 0, replaced by -inf below
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)xr, (short)0, C * 4, 0x00020000);
 #pragma unroll
   for (int u = 0; u < NV; ++u) {
-    const int q = 64 * u + lane;
-    float4 f = make_float4(NI, NI, NI, NI);
-    if (q < C4) f = xr[q];
-    k[u][0] = __float_as_uint(f.x); k[u][1] = __float_as_uint(f.y);
-    k[u][2] = __float_as_uint(f.z); k[u][3] = __float_as_uint(f.w);
+    const auto f = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, u * 1024, 0);
+    k[u][0] = f[0]; k[u][1] = f[1]; k[u][2] = f[2]; k[u][3] = f[3];
   }
   // maximum, NaN / +inf, the block maxima (block 4 u + (lane >> 4) is the
   // 16-lane DPP row of one u: its maximum lands on the row's lane 15), and
@@ -4443,16 +4649,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_
   float xmax = NI;
   bool bad = false;
   unsigned lk = 0u;
+  const int bl4 = blank - 4 * lane;
 #pragma unroll
   for (int u = 0; u < NV; ++u) {
     float lm = NI;
+    const bool inrow = 64 * u + lane < C4;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      const float v = __uint_as_float(k[u][c]);
+      const float v = inrow ? __uint_as_float(k[u][c]) : NI;
       bad |= (v != v) || (v == PI);
       lm = v > lm ? v : lm;
-      const int cl = 4 * (64 * u + lane) + c;
-      k[u][c] = (64 * u + lane < C4 && cl != blank) ? fkey(v) : 0u;
+      // class 4 lane + 256 u + c is the blank iff 256 u + c == bl4 (no class
+      // index per element: kept for the compaction, 80 of them took 80 VGPRs);
+      // bitwise &: no short-circuit branch, so the key takes the value's register
+      const unsigned kv = fkey(v);
+      k[u][c] = (inrow & (256 * u + c != bl4)) ? kv : 0u;
       lk = k[u][c] > lk ? k[u][c] : lk;
     }
     xmax = lm > xmax ? lm : xmax;
@@ -4467,12 +4678,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_
   RowHdr<float> h;
   h.xmax = wave_max_dpp(xmax);
   h.bad = __ballot(bad) != 0ull;
-#ifdef CTCX_FACTS_LOADONLY   // timing experiments only: the row's load and first pass
-  h.ns = 0;
-  h.xout = __uint_as_float(lk);
-  if (lane == 0) *(RowHdr<float>*)pr = h;
-  return;
-#endif
   const int K = kTopK;
   auto unkey = [](unsigned kv) { return kv ^ ((kv >> 31) ? 0x80000000u : 0xFFFFFFFFu); };   // fkey's inverse
   const uint64_t ltm = (1ull << lane) - 1ull;
@@ -4489,6 +4694,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_
   unsigned* cks = cks_all[wv];
   unsigned* cls = cls_all[wv];
   int n = 0;
+  int lb4;   // 4 lane, opaque: recomputed here, not kept from the first pass
+  __asm__ volatile("v_lshlrev_b32 %0, 2, %1" : "=v"(lb4) : "v"(lane));
 #pragma unroll
   for (int u = 0; u < NV; ++u) {
     if (64 * u < C4) {   // uniform
@@ -4504,10 +4711,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_
       int at = n + before;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const int cl = 4 * (64 * u + lane) + c;
+        // label index: class 4 lane + 256 u + c, less one past the blank
         const int j = (in[c] && at < kFactsCompact) ? at : kFactsCompact + lane;
         cks[j] = k[u][c];
-        cls[j] = (unsigned)(cl - (cl > blank ? 1 : 0));
+        cls[j] = (unsigned)(lb4 + (256 * u + c) - (256 * u + c > bl4 ? 1 : 0));
         at += in[c] ? 1 : 0;
       }
 #pragma unroll
@@ -4578,8 +4785,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           if (in[c]) {
-            const int cl = 4 * (64 * u + lane) + c;
-            top[ns + before] = make_uint2(unkey(k[u][c]), (unsigned)(cl - (cl > blank ? 1 : 0)));
+            top[ns + before] = make_uint2(unkey(k[u][c]), (unsigned)(lb4 + (256 * u + c) - (256 * u + c > bl4 ? 1 : 0)));
             ++before;
           }
         }
