@@ -238,6 +238,31 @@ extern "C" int ctcext_phase_counters(ctcext_decoder* d, uint64_t* out, int64_t n
   return CTCEXT_OK;
 }
 
+extern "C" int ctcext_row_facts(ctcext_decoder* d, const void* x, int32_t dtype, int64_t max_time, int64_t batch,
+                                int64_t num_classes, int32_t blank_index, const int32_t* seq_len, void* prep,
+                                void* norm, int64_t* row_bytes) {
+  if (!d || !row_bytes) return fail(CTCEXT_INVALID_ARGUMENT, "null argument");
+  if (dtype != CTCEXT_F32 && dtype != CTCEXT_F64) return fail(CTCEXT_INVALID_ARGUMENT, "dtype");
+  if (max_time < 0 || batch < 0 || num_classes <= 64 || blank_index < 0 || blank_index >= num_classes)
+    return fail(CTCEXT_INVALID_ARGUMENT, "the pre-pass runs for num_classes > 64 and a blank index inside it");
+  const int ts = dtype == CTCEXT_F64 ? 8 : 4;
+  *row_bytes = (int64_t)ctcx::prep_row_bytes(num_classes, ts);
+  if (!prep) return CTCEXT_OK;   // the size query
+  if (!x || !seq_len || !norm) return fail(CTCEXT_INVALID_ARGUMENT, "null argument");
+  Dev& r = d->devs[0];
+  DeviceGuard guard;
+  HIP_OR_FAIL(hipSetDevice(r.device));
+  const hipStream_t st = r.own_stream;
+  if (dtype == CTCEXT_F64)
+    HIP_OR_FAIL(ctcx::launch_row_prep<double>((const double*)x, seq_len, (char*)prep, (double*)norm, max_time, batch,
+                                              num_classes, batch, blank_index, st));
+  else
+    HIP_OR_FAIL(ctcx::launch_row_prep<float>((const float*)x, seq_len, (char*)prep, (float*)norm, max_time, batch,
+                                             num_classes, batch, blank_index, st));
+  HIP_OR_FAIL(hipStreamSynchronize(st));
+  return CTCEXT_OK;
+}
+
 extern "C" int ctcext_get_stats(ctcext_decoder* d, ctcext_stats* s) {
   if (!d || !s) return fail(CTCEXT_INVALID_ARGUMENT, "null argument");
   *s = d->stats;

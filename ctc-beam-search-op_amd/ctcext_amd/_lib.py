@@ -32,7 +32,7 @@ CTCEXT_SCORER_BIGRAM = 1
 # every symbol include/ctcext.h declares
 EXPORTED_SYMBOLS = ("ctcext_create", "ctcext_create_sharded", "ctcext_destroy", "ctcext_validate",
                     "ctcext_decode", "ctcext_decode_sharded", "ctcext_fetch", "ctcext_get_stats",
-                    "ctcext_last_error", "ctcext_max_beam_width", "ctcext_phase_counters")
+                    "ctcext_last_error", "ctcext_max_beam_width", "ctcext_phase_counters", "ctcext_row_facts")
 
 
 class DecodeArgs(ctypes.Structure):
@@ -118,5 +118,9 @@ def load():
     lib.ctcext_max_beam_width.restype = ctypes.c_int32
     lib.ctcext_phase_counters.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
     lib.ctcext_phase_counters.restype = ctypes.c_int
+    lib.ctcext_row_facts.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64,
+                                     ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.POINTER(ctypes.c_int64)]
+    lib.ctcext_row_facts.restype = ctypes.c_int
     _lib = lib
     return lib

@@ -176,6 +176,17 @@ int ctcext_get_stats(ctcext_decoder* dec, ctcext_stats* stats);
  * loops, heap pushes; counts: offer chunks, accepted events, heap pushes). */
 int ctcext_phase_counters(ctcext_decoder* dec, uint64_t* out, int64_t n);
 
+/* Diagnostics (tests): the pre-pass of a decode alone, on device buffers and
+ * the handle's stream, synchronously -- per (t, b) row of inputs
+ * [max_time][batch][num_classes] (num_classes > 64) its record into prep
+ * (*row_bytes each: RowHdr {max, largest non-blank value outside the top
+ * set S, NaN/+inf flag, |S|}, the 64-class block maxima, S as (value bits,
+ * label index) pairs in label order) and its softmax normaliser into norm.
+ * With prep == NULL only *row_bytes is set.  Rows past seq_len are skipped. */
+int ctcext_row_facts(ctcext_decoder* dec, const void* inputs, int32_t dtype, int64_t max_time, int64_t batch,
+                     int64_t num_classes, int32_t blank_index, const int32_t* sequence_length, void* prep,
+                     void* norm, int64_t* row_bytes);
+
 /* Message of the last failing call on this thread ("" if none). */
 const char* ctcext_last_error(void);
 
