@@ -16,4 +16,11 @@ timeout -k 10 200 python -u tools/tier_bench.py > $O/tier.json 2>&1 || exit 1
 TAG=$TAG CFG=cfg5 SEQ=600 bash tools/prep_stats.sh r4p:ab/libr4p.so new: $EXTRA_LIBS || exit 1
 TAG=$TAG CFG=cfg4 SEQ=2000 bash tools/prep_stats.sh r4p4:ab/libr4p.so new4: || exit 1
 TAG=$TAG CFG=cfg5 SEQ=600 bash tools/prep_pmc.sh r4p:ab/libr4p.so new: || exit 1
+if [ "$PHASES" = 1 ]; then
+  export CTCEXT_LIB_PATH=$R/tools/libctcext_phases.so
+  timeout -k 10 120 python3 -u tools/diag_phases.py 128 400 64 1 1000 > $O/phases_cfg4_hw.txt 2>&1 || exit 1
+  CTCEXT_HELPER=0 timeout -k 10 120 python3 -u tools/diag_phases.py 128 400 64 1 1000 > $O/phases_cfg4_onewave.txt 2>&1 || exit 1
+  timeout -k 10 180 python3 -u tools/diag_phases.py 256 100 256 1 5000 > $O/phases_cfg5_hw.txt 2>&1 || exit 1
+  unset CTCEXT_LIB_PATH
+fi
 echo done >> $O/summary.txt
