@@ -1975,7 +1975,10 @@ __device__ __forceinline__ void gather_chunk(const Ctx<T>& cx, int buf, int nb, 
 // events.  A chunk with cqn = 0 ends the frame's grow (gstop: a closed turn).
 // Hand-over as for the score table (kCtlReady / kCtlCons / kCtlDone), plus
 // wave 0's bottom after every chunk (kCtlBot, float bits).
-constexpr int kQSlots = 4;
+#ifndef CTCX_QSLOTS
+#define CTCX_QSLOTS 4
+#endif
+constexpr int kQSlots = CTCX_QSLOTS;   // chunks the helper may gather ahead of wave 0
 constexpr int kCtlBot = 12;
 struct GQ {
   CTCX_LDS uint32_t* e;     // [slot][64]: (branch << 16) | label index
@@ -1990,7 +1993,8 @@ __device__ __forceinline__ GQ gq_carve(CTCX_LDS char* p) {
 }
 
 template <typename T>
-__device__ __forceinline__ void help_gather_chunks(const Ctx<T>& cx, GQ q, int buf, int nb, T norm, T pmax, T bottom) {
+__device__ __forceinline__ void help_gather_chunks(const Ctx<T>& cx, GQ q, int buf, int nb, T norm, T pmax, T bottom,
+                                                   int lead) {
   const int lane = threadIdx.x & 63;
   CTCX_LDS int* m = cx.misc;
   if (ctl_ld(m, kCtlDead) != 0) return;
@@ -2007,7 +2011,7 @@ __device__ __forceinline__ void help_gather_chunks(const Ctx<T>& cx, GQ q, int b
         done = true;
         break;
       }
-      if (c < ctl_ld(m, kCtlCons) + kQSlots) break;
+      if (c < ctl_ld(m, kCtlCons) + lead) break;
       __builtin_amdgcn_s_sleep(CTCX_SLEEP);
     }
     if (done) break;
@@ -2089,7 +2093,13 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
   if constexpr (HW) {
     if (tid >= 64) {
       if constexpr (BIG) {
-        if (nb >= W) help_gather_chunks<T>(cx, gq, buf, nb, norm, pmax, wave_min(lmin));
+        // how far ahead of wave 0 the helper gathers (at most kQSlots chunks):
+        // a chunk gathered early carries offers a later bottom rejects, and at
+        // beams of <= 128 wave 0 runs those chunks faster than the helper
+        // gathers, so one ahead is best there (cfg4 179.3 -> 165.2 ms per
+        // launch, same box); beams of 129..256 gain from the full lead (cfg5:
+        // 1434 ms at 4 ahead, 1437 at 2, 1454 at 1)
+        if (nb >= W) help_gather_chunks<T>(cx, gq, buf, nb, norm, pmax, wave_min(lmin), RN == 1 ? 1 : kQSlots);
       } else {
         help_score_chunks<T>(cx, tb, buf, nb, norm);
       }
@@ -4534,7 +4544,7 @@ __global__ __launch_bounds__(64) void ctcx_row_prep(const T* __restrict__ x, con
 
 // ---------------------------------------------------------------------------
 // ctcx_row_facts: ctcx_row_prep's row facts (RowHdr, block maxima, the top
-// set S) for float rows with C % 4 == 0 and C <= 1024 * NV, with the row in
+// set S) for float rows with C % 4 == 0 and C <= 256 * NV, with the row in
 // registers instead of LDS: lane L holds classes 4 (64 u + L) + c of the row
 // (float4 loads, u < NV, c < 4), all NV loads in flight at once, and every
 // pass over the row (maxima, counts, S) runs on those registers.  A 64-class
@@ -4615,9 +4625,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_
     int64_t B, int C, int64_t xstride, int blank) {
   // per wave: the compact list of (key, label index) in label order, with one
   // dummy slot per lane (its stores are unconditional), and the radix histogram
-  __shared__ unsigned cks_all[4][kFactsCompact + 64];
-  __shared__ unsigned cls_all[4][kFactsCompact + 64];
-  __shared__ unsigned hist_all[4][256];
+  // (NV <= 4, C <= 1024: 16 keys per lane, bisected in registers as cheaply
+  // as a radix select's fixed passes, and no LDS: more waves per SIMD)
+  constexpr bool kRadix = NV > 4;
+  __shared__ unsigned cks_all[4][kRadix ? kFactsCompact + 64 : 1];
+  __shared__ unsigned cls_all[4][kRadix ? kFactsCompact + 64 : 1];
+  __shared__ unsigned hist_all[4][kRadix ? 256 : 1];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t row = (int64_t)blockIdx.x * 4 + wv;
   if (row >= rows) return;   // wave-uniform, and no block barrier below
@@ -4693,12 +4706,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_
   // order is (lane, c) order): a label's slot is the count before it
   unsigned* cks = cks_all[wv];
   unsigned* cls = cls_all[wv];
-  int n = 0;
+  int n = 0;   // keys >= kt
   int lb4;   // 4 lane, opaque: recomputed here, not kept from the first pass
   __asm__ volatile("v_lshlrev_b32 %0, 2, %1" : "=v"(lb4) : "v"(lane));
 #pragma unroll
   for (int u = 0; u < NV; ++u) {
-    if (64 * u < C4) {   // uniform
+    if (kRadix && 64 * u < C4) {   // uniform
       bool in[4];
       int before = 0;
       uint64_t mm[4];
@@ -4724,7 +4737,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (n <= kFactsCompact && (n > K || C - 1 <= K)) {
+  if (kRadix && n <= kFactsCompact && (n > K || C - 1 <= K)) {
     // S from the list: all of it (C - 1 <= K), or the keys above the
     // (K+1)-th largest, found by a radix select over the list
     unsigned v = 0u;
@@ -4744,9 +4757,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_
     h.ns = ns;
     h.xout = v == 0u ? NI : __uint_as_float(unkey(v));
   } else {
-    // the rare shapes: exactly K keys at or above km (S is the list, its
-    // outside maximum taken from the registers), or a list past its capacity
-    // (tau bisected over the row's keys, S from the registers)
+    // NV <= 4, and the rare shapes: exactly K keys at or above km (S is the
+    // list, its outside maximum taken from the registers), or a list past its
+    // capacity (tau bisected over the row's keys, S from the registers)
     auto cnt_ge = [&](unsigned tau) __attribute__((always_inline)) {
       int c2 = 0;
 #pragma unroll
@@ -4755,6 +4768,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_
         for (int c = 0; c < 4; ++c) c2 += k[u][c] >= tau ? 1 : 0;
       return uni(wave_sum_dpp(c2));
     };
+    if constexpr (!kRadix) n = cnt_ge(kt);
     unsigned tau = kt;
     if (n > K) {
       uint64_t lo = kt - 1u, hi = (uint64_t)kmx + 1ull;   // cnt(lo) >= cnt(kt) > K >= cnt(hi) = 0
@@ -5152,7 +5166,7 @@ hipError_t launch_row_prep(const T* x, const int32_t* sl, char* prep, T* norm, i
   if constexpr (sizeof(T) == 4) {
     // float rows of whole float4s (16-byte aligned): the register-resident
     // row facts, then the rows-per-lane normaliser reading their maxima
-    if (C % 4 == 0 && ((uintptr_t)x & 15) == 0 && C <= 1024 * 32) {
+    if (C % 4 == 0 && ((uintptr_t)x & 15) == 0 && C <= 256 * 32) {   // NV <= 32 float4 per lane
       const int c4 = (int)(C / 4);
       hipError_t e;
       if (c4 <= 64) e = launch_row_facts<1>(x, sl, prep, rows, B, (int)C, xstride, blank, s);

@@ -118,9 +118,10 @@ def load():
     lib.ctcext_max_beam_width.restype = ctypes.c_int32
     lib.ctcext_phase_counters.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
     lib.ctcext_phase_counters.restype = ctypes.c_int
-    lib.ctcext_row_facts.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64,
-                                     ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                     ctypes.POINTER(ctypes.c_int64)]
-    lib.ctcext_row_facts.restype = ctypes.c_int
+    if hasattr(lib, "ctcext_row_facts"):   # (diagnostics; absent from builds before it, kept loadable for A/B)
+        lib.ctcext_row_facts.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
+                                         ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]
+        lib.ctcext_row_facts.restype = ctypes.c_int
     _lib = lib
     return lib
