@@ -9,7 +9,7 @@ for r in $(seq $N); do
   for v in "$@"; do
     IFS='|' read -r label envs lib xargs <<< "$v"
     [ -n "$lib" ] && lib="CTCEXT_LIB_PATH=$R/$lib"
-    out=$(cd $R && env $envs $lib timeout -k 10 240 python bench.py --config $CFG --steps 3 --warmup 1 --no-cpu --no-host-io --no-strong $EXTRA $xargs 2>/dev/null | python3 -c 'import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print("%.0f %.2f %.3f" % (d["value"], d["roofline"]["kernel_ms"], d["roofline"].get("prepass_ms") or 0.0))') || exit 1
+    out=$(cd $R && env $envs $lib timeout -k 10 240 python bench.py --config $CFG --steps 3 --warmup 1 --no-cpu --no-host-io --no-strong $EXTRA $xargs 2>/dev/null | python3 -c 'import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print("%.0f %.2f %.3f %.3f %.2f" % (d["value"], d["roofline"]["kernel_ms"], d["roofline"].get("prepass_ms") or 0.0, d["roofline"].get("traceback_ms") or 0.0, d["ms_per_step"]))') || exit 1
     echo "$label $out"
   done
 done
