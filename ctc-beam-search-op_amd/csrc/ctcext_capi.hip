@@ -24,9 +24,9 @@ namespace ctcx {
 template <typename T>
 hipError_t launch_decode(const DecodeParams<T>& p, hipStream_t s);
 template <typename T>
-int ring_frames(const DecodeParams<T>& p, int cus, int cap);
+int ring_frames(const DecodeParams<T>& p, int cus, int cap, int hk);
 template <typename T>
-int use_helper_kernel(const DecodeParams<T>& p);
+int use_helper_kernel(const DecodeParams<T>& p, int hk);
 template <typename T>
 int helper_kind(const DecodeParams<T>& p);
 template <typename T>
@@ -264,11 +264,20 @@ extern "C" int ctcext_row_facts(ctcext_decoder* d, const void* x, int32_t dtype,
 }
 
 extern "C" int ctcext_get_stats(ctcext_decoder* d, ctcext_stats* s) {
+  return ctcext_get_stats_sized(d, s, sizeof(ctcext_stats));
+}
+
+// The struct has grown by appending fields (ctcext.h); a caller built against
+// an older header passes its own sizeof and receives that prefix only.
+extern "C" int ctcext_get_stats_sized(ctcext_decoder* d, ctcext_stats* s, size_t size) {
   if (!d || !s) return fail(CTCEXT_INVALID_ARGUMENT, "null argument");
-  *s = d->stats;
-  s->n_devices = (int32_t)d->devs.size();
+  ctcext_stats v = d->stats;
+  v.n_devices = (int32_t)d->devs.size();
+  memcpy(s, &v, std::min(size, sizeof(ctcext_stats)));
   return CTCEXT_OK;
 }
+
+extern "C" int32_t ctcext_abi_version(void) { return CTCEXT_ABI_VERSION; }
 
 // ---------------------------------------------------------------------------
 // Validation, in the reference's order (kernels.cc:97-139), host only.
@@ -387,7 +396,7 @@ static void shard_bounds(const std::vector<int32_t>& hsl, int n, std::vector<int
 // x/sl point at the shard's first item; xstride is items per frame in x.
 template <typename T>
 static int enqueue_shard(ctcext_decoder* d, Dev& v, bool root, const ctcext_decode_args* a, const T* x,
-                         int64_t xstride, const int32_t* sl) {
+                         int64_t xstride, const int32_t* sl, bool helper_off) {
   const int64_t T_ = a->max_time, C = a->num_classes, B = d->B, Bs = v.nb;
   const int W = a->beam_width, P = a->top_paths;
   const bool prof = (a->flags & CTCEXT_FLAG_PROFILE) != 0;
@@ -452,21 +461,27 @@ static int enqueue_shard(ctcext_decoder* d, Dev& v, bool root, const ctcext_deco
   if (Bs > 0x7fffffffLL || (!gs && (W > ctcx::kMaxRecBeam || C > ctcx::kMaxRecClasses)))
     return fail(CTCEXT_INTERNAL, "shard shape outside the kernel's limits");
   v.ring = 0;
+  // the two-wave kernel: decided once here (the shape's kind, or none when
+  // helper_off), then the ring, the kernel and the traceback's record format
+  // all follow p.helper
+  const int hk = (gs || helper_off) ? 0 : ctcx::helper_kind<T>(p);
+  p.test_flags = (a->flags & CTCEXT_FLAG_TEST_HELPER_DEAD) ? ctcx::kTestHelperDead : 0;
   // the record ring: asked for, or the default of the score-table two-wave kernel
   const bool ring = (a->flags & (CTCEXT_FLAG_RECORD_RING | CTCEXT_FLAG_RING_MIN)) ||
-                    (!(a->flags & CTCEXT_FLAG_NO_RING) && ctcx::helper_kind<T>(p) == 1);
+                    (!(a->flags & CTCEXT_FLAG_NO_RING) && hk == 1);
   if (!gs && ring) {
     if (v.cus == 0 && hipDeviceGetAttribute(&v.cus, hipDeviceAttributeMultiprocessorCount, v.device) != hipSuccess)
       v.cus = 1;
     // CTCEXT_RING_FRAMES (diagnostics): a smaller ring cap than the default 64
     const char* rc = getenv("CTCEXT_RING_FRAMES");
     const int cap = (a->flags & CTCEXT_FLAG_RING_MIN) ? 8 : (rc && atoi(rc) >= 8) ? std::min(atoi(rc), 256) : 64;
-    p.ring = v.ring = ctcx::ring_frames<T>(p, v.cus, cap);
+    p.ring = v.ring = ctcx::ring_frames<T>(p, v.cus, cap, hk);
     if (p.ring > 0) {
       HIP_OR_FAIL(v.foff.ensure(4 * (size_t)(Bs * T_)));
       p.foff = (int32_t*)v.foff.p;
     }
   }
+  p.helper = v.helper = ctcx::use_helper_kernel<T>(p, hk);
   if (gs) {
     p.gstate = (char*)v.gstate.p;
     p.gstate_stride = (int64_t)ctcx::gstate_bytes(W, (int)sizeof(T), scored);
@@ -480,7 +495,6 @@ static int enqueue_shard(ctcext_decoder* d, Dev& v, bool root, const ctcext_deco
   tp.rec = p.rec; tp.item = p.item; tp.seq_len = sl; tp.top_pos = p.top_pos; tp.top_kind = p.top_kind;
   tp.Tmax = T_; tp.B = Bs; tp.W = W; tp.P = P; tp.merge = a->merge_repeated ? 1 : 0;
   tp.blank_label = a->blank_label;
-  v.helper = gs ? 0 : ctcx::use_helper_kernel<T>(p);
   tp.rec_fmt = gs ? ctcx::kRecFmt128 : v.helper == 1 ? ctcx::kRecFmt32 : ctcx::kRecFmt64;
   v.rec_bytes = tp.rec_fmt == ctcx::kRecFmt128 ? 16 : tp.rec_fmt == ctcx::kRecFmt32 ? 4 : 8;
   tp.foff = p.foff;
@@ -494,7 +508,7 @@ static int enqueue_shard(ctcext_decoder* d, Dev& v, bool root, const ctcext_deco
 
 template <typename T>
 static int run_decode(ctcext_decoder* d, const ctcext_decode_args* a, const std::vector<int32_t>& hsl,
-                      hipStream_t root_stream) {
+                      hipStream_t root_stream, bool helper_off) {
   const int64_t T_ = a->max_time, B = a->batch_size, C = a->num_classes;
   const int P = a->top_paths;
   const int ts = (int)sizeof(T);
@@ -542,7 +556,7 @@ static int run_decode(ctcext_decoder* d, const ctcext_decode_args* a, const std:
       xstride = v.nb;
       sl = (const int32_t*)v.sl.p;
     }
-    int rc = enqueue_shard<T>(d, v, i == 0, a, x, xstride, sl);
+    int rc = enqueue_shard<T>(d, v, i == 0, a, x, xstride, sl, helper_off);
     if (rc != CTCEXT_OK) return rc;
   }
 
@@ -609,8 +623,18 @@ static int run_decode(ctcext_decoder* d, const ctcext_decode_args* a, const std:
     d->stats.duplicate_frames += io[b].dup_frames;
     d->stats.records_written += io[b].records;
   }
-  for (int64_t b = 0; b < B; ++b)
-    if (io[b].pad != 0) return fail(CTCEXT_INTERNAL, "decode kernel: a helper-wave hand-over wait timed out");
+  bool dead = false;
+  for (int64_t b = 0; b < B; ++b) dead |= io[b].pad != 0;
+  if (dead) {
+    // a two-wave kernel's hand-over wait ran out of time (~1 s; never in a
+    // correct run): its items' results are incomplete.  The call is decoded
+    // again with the one-wave kernels, unless the caller asked to fail
+    if (helper_off || (a->flags & CTCEXT_FLAG_HELPER_STRICT))
+      return fail(CTCEXT_INTERNAL, "decode kernel: a helper-wave hand-over wait timed out");
+    const int rc = run_decode<T>(d, a, hsl, root_stream, true);
+    d->stats.helper_redecodes += 1;
+    return rc;
+  }
   // TopPaths (decoder.h:240-243) fails on the first item with too few leaves
   for (int64_t b = 0; b < B; ++b)
     if (io[b].n_leaves < P) return fail(CTCEXT_INVALID_ARGUMENT, "Less leaves in the beam search than requested.");
@@ -661,7 +685,11 @@ extern "C" int ctcext_decode_sharded(ctcext_decoder* d, const ctcext_decode_args
   d->sizes.assign((size_t)P, ctcext_path_sizes{0, 0, 0, 0});
   d->stats = ctcext_stats{};
   if (B > 0) {
-    rc = (a->dtype == CTCEXT_F32) ? run_decode<float>(d, a, hsl, s) : run_decode<double>(d, a, hsl, s);
+    // CTCEXT_HELPER=0 (diagnostics): the one-wave kernels; read once per call
+    const char* hv = getenv("CTCEXT_HELPER");
+    const bool helper_off = hv && hv[0] == '0';
+    rc = (a->dtype == CTCEXT_F32) ? run_decode<float>(d, a, hsl, s, helper_off)
+                                  : run_decode<double>(d, a, hsl, s, helper_off);
     if (rc != CTCEXT_OK) return rc;
     const int64_t* r = (const int64_t*)d->h_res.p;
     for (int p = 0; p < P; ++p) {

@@ -1627,7 +1627,19 @@ __device__ __forceinline__ void wsync() {
 #define CTCX_SLEEP 1
 #endif
 constexpr int kTabSlots = CTCX_TAB_SLOTS;   // chunk slots in the ring
-constexpr int kSpinCap = 1 << 16;      // s_sleep(1) rounds before a wait gives up (~4 ms)
+// A hand-over wait gives up after ~1 s of the constant 100 MHz clock
+// (s_memrealtime), whatever the shader clock or the SIMD's other work: only a
+// real deadlock reaches it (a frame's whole chain is ~100 us).  The clock is
+// read on the wait's first round and then every 256 rounds.
+#ifndef CTCX_WAIT_TICKS
+#define CTCX_WAIT_TICKS 100000000ull
+#endif
+__device__ __forceinline__ bool wait_expired(int spin, uint64_t& t0) {
+  if (spin & 255) return false;
+  const uint64_t now = __builtin_amdgcn_s_memrealtime();
+  if (spin == 0) t0 = now;
+  return now - t0 > (uint64_t)(CTCX_WAIT_TICKS);
+}
 struct Tab {
   CTCX_LDS u32x4* a;    // [slot][lane]: score, branch total, packed, candidate back-pointer
   CTCX_LDS float* p;    // [slot][lane]: candidate value
@@ -1639,8 +1651,9 @@ __device__ __forceinline__ Tab tab_carve(CTCX_LDS char* p) {
   t.p = (CTCX_LDS float*)(p + (size_t)kTabSlots * 64 * 16);
   return t;
 }
-// control words in misc[8..11]; kCtlDead (sticky for the kernel): a wait gave
-// up, every later wait returns at once, and the item reports it (ItemOut.pad)
+// control words in misc[8..11]; kCtlDead (sticky for the kernel): a wait ran
+// out of time, every later wait returns at once, wave 0 ends every grow
+// without reading the table or queue, and the item reports it (ItemOut.pad)
 constexpr int kCtlReady = 8, kCtlCons = 9, kCtlDone = 10, kCtlDead = 11;
 __device__ __forceinline__ int ctl_ld(CTCX_LDS int* m, int k) {
   return uni(__hip_atomic_load(&m[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
@@ -1661,9 +1674,10 @@ __device__ __forceinline__ void help_score_chunks(const Ctx<T>& cx, Tab tb, int 
   CTCX_LDS int* m = cx.misc;
   if (ctl_ld(m, kCtlDead) != 0) return;
   for (int c = 0; c < nch; ++c) {
+    uint64_t tw = 0;
     for (int spin = 0;; ++spin) {   // the grow still running, and a free slot
       if (ctl_ld(m, kCtlDone) != 0) return;
-      if (spin > kSpinCap) {
+      if (wait_expired(spin, tw)) {
         __hip_atomic_store(&m[kCtlDead], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         return;
       }
@@ -2004,9 +2018,10 @@ __device__ __forceinline__ void help_gather_chunks(const Ctx<T>& cx, GQ q, int b
   bool gstop = false;
   for (int c = 0;; ++c) {
     bool done = false;
+    uint64_t tw = 0;
     for (int spin = 0;; ++spin) {   // the grow still running, and a free slot
       if (ctl_ld(m, kCtlDone) != 0) { done = true; break; }
-      if (spin > kSpinCap) {
+      if (wait_expired(spin, tw)) {
         __hip_atomic_store(&m[kCtlDead], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         done = true;
         break;
@@ -2262,17 +2277,25 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
             // the slot reads complete with the count (one round trip): otherwise
             // the compiler sinks them below the test, a second round trip
             __asm__ volatile("" ::"v"(ta[0]), "v"(ta[1]), "v"(tpv[0]), "v"(tpv[1]));
-            if (__builtin_expect(uni(rdy) < need && !cx.tabdead, 0)) {
-              // wave 1 is behind (rare): wait for the count, then read again
-              for (int spin = 0;; ++spin) {
+            if (__builtin_expect(uni(rdy) < need || cx.tabdead, 0)) {
+              // wave 1 is behind (rare): wait for the count, then read again.
+              // A wait that runs out of time, or a helper that gave up, ends
+              // this frame's grow here and every later frame's at its first
+              // window: the table's slots are never used then (the host
+              // decodes the call again with the one-wave kernel, or fails it)
+              uint64_t tw = 0;
+              for (int spin = 0; !cx.tabdead; ++spin) {
                 spins = spin + 1;
                 __builtin_amdgcn_s_sleep(CTCX_SLEEP);
                 if (ctl_ld(cx.misc, kCtlReady) >= need) break;
-                if (spin > kSpinCap) {   // never in a correct run: give up for the rest of the kernel
+                if (ctl_ld(cx.misc, kCtlDead) != 0 || wait_expired(spin, tw)) {   // never in a correct run
                   cx.tabdead = 1;
                   __hip_atomic_store(&cx.misc[kCtlDead], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                  break;
                 }
+              }
+              if (cx.tabdead) {
+                stop = true;
+                break;
               }
               __asm__ volatile("" ::: "memory");
               ta[0] = tb.a[s0];
@@ -2577,10 +2600,15 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
           gqp = gq.e[slot * 64 + (lane > 0 ? lane - 1 : 0)];
           __asm__ volatile("" ::"v"(h0), "v"(h1), "v"(h2), "v"(h3), "v"(gqe), "v"(gqp));   // one round trip
           if (__builtin_expect(uni(rdy) <= gqc && !cx.tabdead, 0)) {
-            for (int spin = 0;; ++spin) {   // wave 1 is behind: wait for the count, then read again
+            // wave 1 is behind: wait for the count, then read again (a wait that
+            // runs out of time, or a helper that gave up, takes cqn = 0 below:
+            // the grow of this frame and of every later one ends, no queue
+            // slot is used)
+            uint64_t tw = 0;
+            for (int spin = 0;; ++spin) {
               __builtin_amdgcn_s_sleep(CTCX_SLEEP);
               if (ctl_ld(cx.misc, kCtlReady) > gqc) break;
-              if (spin > kSpinCap) {   // never in a correct run: give up for the rest of the kernel
+              if (ctl_ld(cx.misc, kCtlDead) != 0 || wait_expired(spin, tw)) {   // never in a correct run
                 cx.tabdead = 1;
                 __hip_atomic_store(&cx.misc[kCtlDead], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 break;
@@ -3813,7 +3841,9 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
   int buf = 0;
   if (tid < 32) cx.etab[tid] = gm::exp2f_tab(tid);
   if (tid == 0) {
-    cx.misc[kCtlDead] = 0;
+    // (tests: kTestHelperDead starts the helper out as if its first wait had
+    // run out of time, so the failure path runs without a hang)
+    cx.misc[kCtlDead] = (HW && (prm.test_flags & kTestHelperDead)) ? 1 : 0;
     cx.lab[0][0] = -1; cx.par[0][0] = -1; cx.flg[0][0] = F_ROOT;
     cx.ot[0][0] = T(0); cx.ob[0][0] = T(0); cx.ol[0][0] = ninf<T>();
     cx.cb[0][0] = T(0); cx.cn[0][0] = T(0);
@@ -5072,15 +5102,14 @@ static hipError_t launch_decode_r(const DecodeParams<T>& p, hipStream_t s) {
   return p.C > 64 ? launch_decode_c<T, RN, WC, true, SC>(p, s) : launch_decode_c<T, RN, WC, false, SC>(p, s);
 }
 
-// The two-wave kernels (helper_kind; 0: none): 1 the score table (float,
-// beams <= 128, C <= 64; 4-byte records), 2 the gather queue (float, beams <=
-// 256, C > 64).  The base scorer only.  CTCEXT_HELPER=0 (diagnostics): the
-// one-wave kernels instead.
+// The two-wave kernel a shape can run (helper_kind; 0: none): 1 the score
+// table (float, beams <= 128, C <= 64; 4-byte records), 2 the gather queue
+// (float, beams <= 256, C > 64).  The base scorer only.  The host decides once
+// per call (enqueue_shard), with CTCEXT_HELPER=0 (diagnostics) or the
+// one-wave re-decode after a helper timeout choosing none.
 template <typename T>
 int helper_kind(const DecodeParams<T>& p) {
   if (sizeof(T) != 4 || p.scorer_tab != nullptr) return 0;
-  const char* hv = getenv("CTCEXT_HELPER");
-  if (hv && hv[0] == '0') return 0;
   if (p.C <= kRec32MaxClasses) return p.W <= kRec32MaxBeam ? 1 : 0;
   return p.W <= 256 ? 2 : 0;
 }
@@ -5092,17 +5121,17 @@ size_t pre_ring_lds_bytes(const DecodeParams<T>& p, int hk, int wc) {
   const size_t b = (decode_lds_bytes(wc, p.C, (int)sizeof(T), p.scorer_tab != nullptr) + 15) & ~(size_t)15;
   return hk == 1 ? b + tab_lds_bytes() : hk == 2 ? b + gq_lds_bytes() : b;
 }
-// the two-wave kernel this call runs (0: none): its layout and ring must fit
+// the two-wave kernel this call runs (0: none), given the kind the host chose
+// (hk): its layout and ring must fit
 template <typename T>
-int use_helper_kernel(const DecodeParams<T>& p) {
-  const int hk = helper_kind(p);
+int use_helper_kernel(const DecodeParams<T>& p, int hk) {
   if (hk == 0) return 0;
   size_t b = pre_ring_lds_bytes(p, hk, helper_wc(p.W));
   if (p.ring > 0) b = ((b + 15) & ~(size_t)15) + ring_lds_bytes(p.ring, p.W, hk == 1 ? 4 : 8);
   return b <= kLdsBytes ? hk : 0;
 }
-template int use_helper_kernel<float>(const DecodeParams<float>&);
-template int use_helper_kernel<double>(const DecodeParams<double>&);
+template int use_helper_kernel<float>(const DecodeParams<float>&, int);
+template int use_helper_kernel<double>(const DecodeParams<double>&, int);
 template int helper_kind<float>(const DecodeParams<float>&);
 template int helper_kind<double>(const DecodeParams<double>&);
 
@@ -5120,7 +5149,9 @@ hipError_t launch_decode(const DecodeParams<T>& p, hipStream_t s) {
   }
   auto fits = [&](int wc) { return decode_lds_bytes(wc, p.C, (int)sizeof(T), false) <= kLdsBytes; };
   if constexpr (sizeof(T) == 4) {
-    const int hk = use_helper_kernel(p);
+    // p.helper: the host's one decision (use_helper_kernel), checked again here
+    const int hk = p.helper;
+    if (hk != 0 && use_helper_kernel(p, hk) != hk) return hipErrorInvalidValue;
     if (hk == 1) return launch_decode_c<float, 1, 128, false, BaseBeamScorer<float>, true>(p, s);
     if (hk == 2)
       return p.W <= 128 ? launch_decode_c<float, 1, 128, true, BaseBeamScorer<float>, true>(p, s)
@@ -5140,14 +5171,13 @@ template hipError_t launch_decode<double>(const DecodeParams<double>&, hipStream
 // the layout alone already takes more than half a CU), else within 80 KB, so
 // two items still share a CU.  The stream offsets (foff) are int32.
 template <typename T>
-int ring_frames(const DecodeParams<T>& p, int cus, int cap) {
+int ring_frames(const DecodeParams<T>& p, int cus, int cap, int hk) {
   const bool scored = p.scorer_tab != nullptr;
   auto fits = [&](int wc) { return decode_lds_bytes(wc, p.C, (int)sizeof(T), scored) <= kLdsBytes; };
   const int wcap = (p.W <= 128 && fits(128)) ? 128 : (p.W > 128 && p.W <= 256 && fits(256)) ? 256 : p.W;
   if ((int64_t)p.Tmax * p.W > 0x7fffffffLL) return 0;
-  // the two-wave kernel, when its layout and a ring fit (the score table's
-  // records are 4 bytes)
-  int hk = helper_kind(p);
+  // the two-wave kernel the host chose (hk), when its layout and a ring fit
+  // (the score table's records are 4 bytes)
   if (hk && pre_ring_lds_bytes(p, hk, helper_wc(p.W)) + ring_lds_bytes(8, p.W, hk == 1 ? 4 : 8) > kLdsBytes) hk = 0;
   const int rb = hk == 1 ? 4 : 8;
   const size_t base = pre_ring_lds_bytes(p, hk, hk ? helper_wc(p.W) : wcap);
@@ -5163,8 +5193,8 @@ int ring_frames(const DecodeParams<T>& p, int cus, int cap) {
   }
   return 0;
 }
-template int ring_frames<float>(const DecodeParams<float>&, int, int);
-template int ring_frames<double>(const DecodeParams<double>&, int, int);
+template int ring_frames<float>(const DecodeParams<float>&, int, int, int);
+template int ring_frames<double>(const DecodeParams<double>&, int, int, int);
 
 template <int NV>
 static hipError_t launch_row_facts(const float* x, const int32_t* sl, char* prep, int64_t rows, int64_t B, int C,

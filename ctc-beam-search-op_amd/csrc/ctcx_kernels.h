@@ -84,7 +84,7 @@ struct ItemOut {
   int32_t dup_frames;     // frames whose beam held one entry twice (-inf logits)
   int32_t why_nonfinite;  // literal replays caused by a non-finite logit or total
   int32_t why_fill;       // ... by the beam filling up mid-frame
-  int32_t pad;            // two-wave kernels: nonzero if a helper hand-over wait gave up
+  int32_t pad;            // two-wave kernels: nonzero if a helper hand-over wait ran out of time
   int64_t records;        // records written to HBM (all of them without the record ring; T * W can pass 2^31)
 };
 static_assert(sizeof(ItemOut) == 32, "ItemOut layout");
@@ -144,7 +144,14 @@ struct DecodeParams {
   // compacted stream at rec + b * Tmax * W, frame t's from foff[b][t] on
   int32_t ring;
   int32_t* foff;            // [B][Tmax]
+  // the two-wave kernel this launch runs (0: the one-wave kernel; 1: score
+  // table; 2: gather queue), decided once per call on the host
+  // (use_helper_kernel): the kernel, the ring's record size and the
+  // traceback's record format all follow this one value
+  int32_t helper;
+  int32_t test_flags;       // kTestHelperDead: the helper wave starts out "timed out" (tests only)
 };
+constexpr int32_t kTestHelperDead = 1;
 
 struct TraceParams {
   const Rec* rec;

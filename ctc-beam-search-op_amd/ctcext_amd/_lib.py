@@ -26,13 +26,17 @@ CTCEXT_FLAG_GLOBAL_STATE = 8   # testing: the global-state tier whatever the sha
 CTCEXT_FLAG_RECORD_RING = 16   # beam records kept in an LDS ring; only the reachable ones written to HBM
 CTCEXT_FLAG_RING_MIN = 32      # testing: the record ring at 8 frames (short items flush); implies RECORD_RING
 CTCEXT_FLAG_NO_RING = 64       # every beam record to HBM (the ring is the default for the score-table kernel)
+CTCEXT_FLAG_HELPER_STRICT = 128     # a helper hand-over timeout fails the call instead of a one-wave re-decode
+CTCEXT_FLAG_TEST_HELPER_DEAD = 256  # testing: the helper wave starts out timed out
+CTCEXT_ABI_VERSION = 5
 CTCEXT_SCORER_BASE = 0
 CTCEXT_SCORER_BIGRAM = 1
 
 # every symbol include/ctcext.h declares
 EXPORTED_SYMBOLS = ("ctcext_create", "ctcext_create_sharded", "ctcext_destroy", "ctcext_validate",
                     "ctcext_decode", "ctcext_decode_sharded", "ctcext_fetch", "ctcext_get_stats",
-                    "ctcext_last_error", "ctcext_max_beam_width", "ctcext_phase_counters", "ctcext_row_facts")
+                    "ctcext_last_error", "ctcext_max_beam_width", "ctcext_phase_counters", "ctcext_row_facts",
+                    "ctcext_get_stats_sized", "ctcext_abi_version")
 
 
 class DecodeArgs(ctypes.Structure):
@@ -73,7 +77,7 @@ class Stats(ctypes.Structure):
                 ("traceback_ms", ctypes.c_double), ("n_devices", ctypes.c_int32),
                 ("tier", ctypes.c_int32), ("ring_frames", ctypes.c_int32),
                 ("records_written", ctypes.c_int64), ("record_bytes", ctypes.c_int32),
-                ("helper", ctypes.c_int32)]
+                ("helper", ctypes.c_int32), ("helper_redecodes", ctypes.c_int32), ("pad_", ctypes.c_int32)]
 
 
 _lib = None
@@ -112,6 +116,11 @@ def load():
     lib.ctcext_fetch.restype = ctypes.c_int
     lib.ctcext_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(Stats)]
     lib.ctcext_get_stats.restype = ctypes.c_int
+    if hasattr(lib, "ctcext_get_stats_sized"):   # (ABI 5; older builds stay loadable for A/B runs)
+        lib.ctcext_get_stats_sized.argtypes = [ctypes.c_void_p, ctypes.POINTER(Stats), ctypes.c_size_t]
+        lib.ctcext_get_stats_sized.restype = ctypes.c_int
+        lib.ctcext_abi_version.argtypes = []
+        lib.ctcext_abi_version.restype = ctypes.c_int32
     lib.ctcext_last_error.argtypes = []
     lib.ctcext_last_error.restype = ctypes.c_char_p
     lib.ctcext_max_beam_width.argtypes = [ctypes.c_int64, ctypes.c_int32]
@@ -125,3 +134,10 @@ def load():
         lib.ctcext_row_facts.restype = ctypes.c_int
     _lib = lib
     return lib
+
+
+def get_stats(lib, handle, st):
+    """Fill Stats st from the last decode on handle (only the prefix an older build knows)."""
+    if hasattr(lib, "ctcext_get_stats_sized"):
+        return lib.ctcext_get_stats_sized(handle, ctypes.byref(st), ctypes.sizeof(st))
+    return lib.ctcext_get_stats(handle, ctypes.byref(st))

@@ -106,8 +106,8 @@ class Decoder:
 
     def stats(self):
         s = _lib.Stats()
-        self.lib.ctcext_get_stats(self.handle, ctypes.byref(s))
-        return {k: getattr(s, k) for k, _ in _lib.Stats._fields_}
+        _lib.get_stats(self.lib, self.handle, s)
+        return {k: getattr(s, k) for k, _ in _lib.Stats._fields_ if k != "pad_"}
 
     # -- phase 1 ---------------------------------------------------------
     def decode(self, args):

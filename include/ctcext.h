@@ -22,6 +22,7 @@
 #ifndef CTCEXT_H_
 #define CTCEXT_H_
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -58,8 +59,21 @@ enum {
                                       beam_width <= 128, num_classes <= 64); opt-in elsewhere */
   CTCEXT_FLAG_RING_MIN = 32,       /* testing: the record ring at its smallest (8 frames), so short
                                       items flush; implies CTCEXT_FLAG_RECORD_RING */
-  CTCEXT_FLAG_NO_RING = 64         /* write every beam record to HBM (no record ring) */
+  CTCEXT_FLAG_NO_RING = 64,        /* write every beam record to HBM (no record ring) */
+  CTCEXT_FLAG_HELPER_STRICT = 128, /* a two-wave kernel's hand-over wait that runs out of time
+                                      (~1 s; never in a correct run) fails the call with
+                                      CTCEXT_INTERNAL instead of decoding it again with the
+                                      one-wave kernels (ctcext_stats.helper_redecodes) */
+  CTCEXT_FLAG_TEST_HELPER_DEAD = 256 /* testing: the helper wave starts out as if its first
+                                      wait had run out of time (the failure path, no hang) */
 };
+
+/* Version of this header's structs and entry points.  ctcext_stats only ever
+ * grows at its end: callers built against an older header use
+ * ctcext_get_stats_sized with their sizeof.
+ *   4: ctcext_stats.record_bytes, .helper     5: .helper_redecodes,
+ *      ctcext_get_stats_sized, ctcext_abi_version, the HELPER_STRICT flag */
+#define CTCEXT_ABI_VERSION 5
 
 typedef struct ctcext_decoder ctcext_decoder;
 
@@ -133,6 +147,10 @@ typedef struct {
                                       num_classes <= 64) */
   int32_t helper;                  /* last decode: the two-wave kernel that ran (0: the one-wave
                                       kernel; 1: score-table helper; 2: gather-queue helper) */
+  int32_t helper_redecodes;        /* last decode: 1 if a two-wave kernel's hand-over wait ran
+                                      out of time and the call was decoded again with the
+                                      one-wave kernels (helper is then 0) */
+  int32_t pad_;
 } ctcext_stats;
 
 /* Handle lifetime.  A handle owns a HIP stream and a grow-only device
@@ -168,7 +186,14 @@ int ctcext_decode_sharded(ctcext_decoder* dec, const ctcext_decode_args* args, c
 /* Phase 2 (StoreAllDecodedSequences + log_probability).  Synchronous. */
 int ctcext_fetch(ctcext_decoder* dec, const ctcext_outputs* out);
 
+/* Statistics of the last decode.  ctcext_get_stats fills this header's whole
+ * struct; ctcext_get_stats_sized fills the first `size` bytes only (a caller
+ * built against an older header passes its sizeof(ctcext_stats)). */
 int ctcext_get_stats(ctcext_decoder* dec, ctcext_stats* stats);
+int ctcext_get_stats_sized(ctcext_decoder* dec, ctcext_stats* stats, size_t size);
+
+/* CTCEXT_ABI_VERSION of the library. */
+int32_t ctcext_abi_version(void);
 
 /* Diagnostics: copies the [batch][16] phase counters of the last decode run
  * with CTCEXT_FLAG_PHASES (cycles: row load, recursion, grow, extract, commit,

@@ -46,6 +46,30 @@ def test_library_exports_every_declared_symbol():
         assert ctypes.cast(getattr(lib, name), ctypes.c_void_p).value
 
 
+def test_abi_structs_match_header(tmp_path):
+    """The ctypes mirrors of ctcext_stats / ctcext_decode_args have the C
+    header's size and field offsets (gcc on include/ctcext.h), and the library
+    reports the header's ABI version."""
+    import subprocess
+    src = tmp_path / "abi.c"
+    fields = {"ctcext_stats": _lib.Stats, "ctcext_decode_args": _lib.DecodeArgs}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "ctcext.h"', "int main(void) {"]
+    for cname, py in fields.items():
+        lines.append('printf("%%s size %%zu\\n", "%s", sizeof(%s));' % (cname, cname))
+        for f, _ in py._fields_:
+            lines.append('printf("%%s %%s %%zu\\n", "%s", "%s", offsetof(%s, %s));' % (cname, f, cname, f))
+    lines.append('printf("abi %d\\n", CTCEXT_ABI_VERSION); return 0; }')
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "abi"
+    subprocess.check_call(["gcc", "-I", os.path.dirname(HEADER), str(src), "-o", str(exe)])
+    got = dict(l.rsplit(" ", 1) for l in subprocess.check_output([str(exe)]).decode().splitlines())
+    for cname, py in fields.items():
+        assert int(got["%s size" % cname]) == ctypes.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert int(got["%s %s" % (cname, f)]) == getattr(py, f).offset, (cname, f)
+    assert int(got["abi"]) == _lib.CTCEXT_ABI_VERSION == _lib.load().ctcext_abi_version()
+
+
 def test_every_shape_validates():
     # no shape limit of its own below the 32-bit indices: num_classes above the
     # 8-byte record (65535) and beams past the LDS tier validate (they decode

@@ -682,3 +682,42 @@ def test_one_wave_kernels_random_families(one_wave):
     _run_random(9104, 30, flags=RMIN)
     _run_random(9105, 10, T_max=40, B_max=2, C_min=3, C_max=40, W_min=129, W_max=256)
     _run_random(9106, 8, T_max=30, B_max=2, C_min=65, C_max=500, W_min=129, W_max=256, ties=True)
+
+
+# ---- the two-wave kernels' failure path (ctcx_decode.hip wait_expired,
+# kCtlDead): a hand-over wait that runs out of time (~1 s of the 100 MHz
+# clock) ends every later grow without reading the table or queue, and the
+# host decodes the call again with the one-wave kernels -- or, with
+# CTCEXT_FLAG_HELPER_STRICT, fails it.  CTCEXT_FLAG_TEST_HELPER_DEAD starts the
+# helper out timed out, so both paths run without a real deadlock or a hang.
+
+DEAD = _lib.CTCEXT_FLAG_TEST_HELPER_DEAD
+
+
+@pytest.mark.parametrize("shape", [(300, 3, 29, 128, 3), (120, 2, 1000, 64, 2), (60, 2, 700, 200, 1)])
+def test_helper_timeout_strict_fails_cleanly(shape):
+    T, B, C, W, P = shape
+    rng = np.random.default_rng(C + W)
+    x = rng.standard_normal((T, B, C)).astype(np.float32)
+    sl = np.full(B, T, np.int32)
+    with pytest.raises(ctcext_amd.InternalError) as ei:
+        ctcext_amd.ctc_ext_beam_search_decoder(x, sl, W, P, merge_repeated=True,
+                                               flags=DEAD | _lib.CTCEXT_FLAG_HELPER_STRICT)
+    assert ei.value.error_code == _lib.CTCEXT_INTERNAL
+    assert "hand-over wait timed out" in str(ei.value)
+    # the handle stays usable: the next call decodes normally
+    out = ctcext_amd.ctc_ext_beam_search_decoder(x, sl, W, P, merge_repeated=True)
+    compare(out, oracle.decode(x, sl, W, P, True), P)
+    assert _stats()["helper"] in (1, 2) and _stats()["helper_redecodes"] == 0
+
+
+@pytest.mark.parametrize("shape", [(300, 3, 29, 128, 3), (120, 2, 1000, 64, 2), (60, 2, 700, 200, 1)])
+def test_helper_timeout_redecodes_one_wave(shape):
+    T, B, C, W, P = shape
+    rng = np.random.default_rng(C * W)
+    x = rng.standard_normal((T, B, C)).astype(np.float32)
+    sl = np.full(B, T, np.int32)
+    out = ctcext_amd.ctc_ext_beam_search_decoder(x, sl, W, P, merge_repeated=True, flags=DEAD)
+    st = _stats()
+    assert st["helper_redecodes"] == 1 and st["helper"] == 0, st
+    compare(out, oracle.decode(x, sl, W, P, True), P)
