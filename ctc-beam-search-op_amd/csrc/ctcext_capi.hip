@@ -28,7 +28,7 @@ int ring_frames(const DecodeParams<T>& p, int cus, int cap, int hk);
 template <typename T>
 int use_helper_kernel(const DecodeParams<T>& p, int hk);
 template <typename T>
-int helper_kind(const DecodeParams<T>& p);
+int helper_kind(const DecodeParams<T>& p, int mode);
 template <typename T>
 hipError_t launch_row_norm(const T* x, const int32_t* sl, T* norm, int64_t T_, int64_t B, int64_t C,
                            int64_t xstride, hipStream_t s);
@@ -43,6 +43,9 @@ hipError_t launch_pack(const PackParams& pp, hipStream_t s);
 hipError_t ctcx_gstate_launch_decode(const void* p, int is_f64, int scored, hipStream_t s);
 
 static thread_local std::string g_err;
+
+// the two-wave kernels a call runs by default (ctcx::helper_kind's mode)
+constexpr int kDefaultHelperMode = ctcx::kHelperLegacy;
 
 static int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -396,7 +399,7 @@ static void shard_bounds(const std::vector<int32_t>& hsl, int n, std::vector<int
 // x/sl point at the shard's first item; xstride is items per frame in x.
 template <typename T>
 static int enqueue_shard(ctcext_decoder* d, Dev& v, bool root, const ctcext_decode_args* a, const T* x,
-                         int64_t xstride, const int32_t* sl, bool helper_off) {
+                         int64_t xstride, const int32_t* sl, int helper_mode) {
   const int64_t T_ = a->max_time, C = a->num_classes, B = d->B, Bs = v.nb;
   const int W = a->beam_width, P = a->top_paths;
   const bool prof = (a->flags & CTCEXT_FLAG_PROFILE) != 0;
@@ -464,11 +467,11 @@ static int enqueue_shard(ctcext_decoder* d, Dev& v, bool root, const ctcext_deco
   // the two-wave kernel: decided once here (the shape's kind, or none when
   // helper_off), then the ring, the kernel and the traceback's record format
   // all follow p.helper
-  const int hk = (gs || helper_off) ? 0 : ctcx::helper_kind<T>(p);
+  const int hk = gs ? 0 : ctcx::helper_kind<T>(p, helper_mode);
   p.test_flags = (a->flags & CTCEXT_FLAG_TEST_HELPER_DEAD) ? ctcx::kTestHelperDead : 0;
   // the record ring: asked for, or the default of the score-table two-wave kernel
   const bool ring = (a->flags & (CTCEXT_FLAG_RECORD_RING | CTCEXT_FLAG_RING_MIN)) ||
-                    (!(a->flags & CTCEXT_FLAG_NO_RING) && hk == 1);
+                    (!(a->flags & CTCEXT_FLAG_NO_RING) && ctcx::helper_rec32(hk, C));
   if (!gs && ring) {
     if (v.cus == 0 && hipDeviceGetAttribute(&v.cus, hipDeviceAttributeMultiprocessorCount, v.device) != hipSuccess)
       v.cus = 1;
@@ -495,7 +498,7 @@ static int enqueue_shard(ctcext_decoder* d, Dev& v, bool root, const ctcext_deco
   tp.rec = p.rec; tp.item = p.item; tp.seq_len = sl; tp.top_pos = p.top_pos; tp.top_kind = p.top_kind;
   tp.Tmax = T_; tp.B = Bs; tp.W = W; tp.P = P; tp.merge = a->merge_repeated ? 1 : 0;
   tp.blank_label = a->blank_label;
-  tp.rec_fmt = gs ? ctcx::kRecFmt128 : v.helper == 1 ? ctcx::kRecFmt32 : ctcx::kRecFmt64;
+  tp.rec_fmt = gs ? ctcx::kRecFmt128 : ctcx::helper_rec32(v.helper, C) ? ctcx::kRecFmt32 : ctcx::kRecFmt64;
   v.rec_bytes = tp.rec_fmt == ctcx::kRecFmt128 ? 16 : tp.rec_fmt == ctcx::kRecFmt32 ? 4 : 8;
   tp.foff = p.foff;
   tp.seq = (int32_t*)v.seq.p;
@@ -508,7 +511,7 @@ static int enqueue_shard(ctcext_decoder* d, Dev& v, bool root, const ctcext_deco
 
 template <typename T>
 static int run_decode(ctcext_decoder* d, const ctcext_decode_args* a, const std::vector<int32_t>& hsl,
-                      hipStream_t root_stream, bool helper_off) {
+                      hipStream_t root_stream, int helper_mode) {
   const int64_t T_ = a->max_time, B = a->batch_size, C = a->num_classes;
   const int P = a->top_paths;
   const int ts = (int)sizeof(T);
@@ -556,7 +559,7 @@ static int run_decode(ctcext_decoder* d, const ctcext_decode_args* a, const std:
       xstride = v.nb;
       sl = (const int32_t*)v.sl.p;
     }
-    int rc = enqueue_shard<T>(d, v, i == 0, a, x, xstride, sl, helper_off);
+    int rc = enqueue_shard<T>(d, v, i == 0, a, x, xstride, sl, helper_mode);
     if (rc != CTCEXT_OK) return rc;
   }
 
@@ -629,9 +632,9 @@ static int run_decode(ctcext_decoder* d, const ctcext_decode_args* a, const std:
     // a two-wave kernel's hand-over wait ran out of time (~1 s; never in a
     // correct run): its items' results are incomplete.  The call is decoded
     // again with the one-wave kernels, unless the caller asked to fail
-    if (helper_off || (a->flags & CTCEXT_FLAG_HELPER_STRICT))
+    if (helper_mode == ctcx::kHelperNone || (a->flags & CTCEXT_FLAG_HELPER_STRICT))
       return fail(CTCEXT_INTERNAL, "decode kernel: a helper-wave hand-over wait timed out");
-    const int rc = run_decode<T>(d, a, hsl, root_stream, true);
+    const int rc = run_decode<T>(d, a, hsl, root_stream, ctcx::kHelperNone);
     d->stats.helper_redecodes += 1;
     return rc;
   }
@@ -685,11 +688,14 @@ extern "C" int ctcext_decode_sharded(ctcext_decoder* d, const ctcext_decode_args
   d->sizes.assign((size_t)P, ctcext_path_sizes{0, 0, 0, 0});
   d->stats = ctcext_stats{};
   if (B > 0) {
-    // CTCEXT_HELPER=0 (diagnostics): the one-wave kernels; read once per call
+    // CTCEXT_HELPER (diagnostics, read once per call): 0 the one-wave kernels,
+    // 1 the score table / unscored gather queue, 3 the scored gather queue
     const char* hv = getenv("CTCEXT_HELPER");
-    const bool helper_off = hv && hv[0] == '0';
-    rc = (a->dtype == CTCEXT_F32) ? run_decode<float>(d, a, hsl, s, helper_off)
-                                  : run_decode<double>(d, a, hsl, s, helper_off);
+    const int helper_mode = !hv || !hv[0] ? kDefaultHelperMode
+                            : hv[0] == '0' ? ctcx::kHelperNone
+                            : hv[0] == '3' ? ctcx::kHelperScored : ctcx::kHelperLegacy;
+    rc = (a->dtype == CTCEXT_F32) ? run_decode<float>(d, a, hsl, s, helper_mode)
+                                  : run_decode<double>(d, a, hsl, s, helper_mode);
     if (rc != CTCEXT_OK) return rc;
     const int64_t* r = (const int64_t*)d->h_res.p;
     for (int p = 0; p < P; ++p) {

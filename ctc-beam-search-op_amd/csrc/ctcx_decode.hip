@@ -1630,14 +1630,15 @@ constexpr int kTabSlots = CTCX_TAB_SLOTS;   // chunk slots in the ring
 // A hand-over wait gives up after ~1 s of the constant 100 MHz clock
 // (s_memrealtime), whatever the shader clock or the SIMD's other work: only a
 // real deadlock reaches it (a frame's whole chain is ~100 us).  The clock is
-// read on the wait's first round and then every 256 rounds.
+// first read after 256 rounds (the common short waits never touch it), then
+// every 256 rounds.
 #ifndef CTCX_WAIT_TICKS
 #define CTCX_WAIT_TICKS 100000000ull
 #endif
 __device__ __forceinline__ bool wait_expired(int spin, uint64_t& t0) {
-  if (spin & 255) return false;
+  if ((spin & 255) != 255) return false;
   const uint64_t now = __builtin_amdgcn_s_memrealtime();
-  if (spin == 0) t0 = now;
+  if (spin == 255) t0 = now;
   return now - t0 > (uint64_t)(CTCX_WAIT_TICKS);
 }
 struct Tab {
@@ -1994,16 +1995,211 @@ __device__ __forceinline__ void gather_chunk(const Ctx<T>& cx, int buf, int nb, 
 #endif
 constexpr int kQSlots = CTCX_QSLOTS;   // chunks the helper may gather ahead of wave 0
 constexpr int kCtlBot = 12;
+// The scored form (SQ kernels: beams <= 128, any C): the helper also scores
+// each gathered offer, as the score table does, so wave 0 reads a chunk's
+// offers ready to push (per lane: score, branch total, packed (branch |
+// (branch child + 1) << 8 | label << 16), the child's label-ending candidate
+// (back-pointer; value in p)).  Wave 0 reads only what events change (bst).
 struct GQ {
-  CTCX_LDS uint32_t* e;     // [slot][64]: (branch << 16) | label index
+  CTCX_LDS uint32_t* e;     // [slot][64]: (branch << 16) | label index (unscored)
   CTCX_LDS int* h;          // [slot][4]: cqn, span start (branch, label index), gstop
+  CTCX_LDS u32x4* a;        // [slot][64]: scored offers (SQ)
+  CTCX_LDS float* p;        // [slot][64]: their candidate values (SQ)
 };
-__host__ __device__ inline size_t gq_lds_bytes() { return (size_t)kQSlots * (64 * 4 + 16); }
+__host__ __device__ inline size_t gq_lds_bytes(bool scored = false) {
+  return (size_t)kQSlots * ((scored ? 64 * 20 : 64 * 4) + 16);
+}
+template <bool SCORED>
 __device__ __forceinline__ GQ gq_carve(CTCX_LDS char* p) {
-  GQ q;
-  q.e = (CTCX_LDS uint32_t*)p;
-  q.h = (CTCX_LDS int*)(p + (size_t)kQSlots * 64 * 4);
+  GQ q{};
+  if constexpr (SCORED) {
+    q.a = (CTCX_LDS u32x4*)p;
+    q.p = (CTCX_LDS float*)(p + (size_t)kQSlots * 64 * 16);
+    q.h = (CTCX_LDS int*)(p + (size_t)kQSlots * 64 * 20);
+  } else {
+    q.e = (CTCX_LDS uint32_t*)p;
+    q.h = (CTCX_LDS int*)(p + (size_t)kQSlots * 64 * 4);
+  }
   return q;
+}
+__device__ __forceinline__ uint32_t sq_pack(int i, int cw, int l) {
+  return (uint32_t)i | ((uint32_t)(cw + 1) << 8) | ((uint32_t)l << 16);
+}
+
+// One offer's scored fields, from the frame-start state only (what the
+// score table holds): its score (decoder.h:166-171), its branch's total, the
+// branch child it re-offers (GetChild finds it; -1: none) and the child's
+// label-ending alignment candidate (decoder.h:172-185).  v: a real offer
+// (others skip the child walk).
+template <typename T>
+__device__ __forceinline__ void sq_score(const Ctx<T>& cx, int buf, T norm, bool v, int i, int l, T& s, T& bt,
+                                         int& cw, Best<T>& cd) {
+  const T NI = ninf<T>();
+  const int bl = sel(cx.lab, buf)[i];
+  const int bflg = sel(cx.flg, buf)[i];
+  bt = sel(cx.ot, buf)[i];
+  const T bob = sel(cx.ob, buf)[i];
+  const int hd = cx.head[i];
+  const T bcb = sel(cx.cb, buf)[i], bcn = sel(cx.cn, buf)[i];
+  const T p = cx.row[l] - norm;
+  s = p + ((l == bl) ? bob : bt);
+  cw = -1;
+  for (int k = v ? hd : -1; __ballot(k >= 0);) {
+    int nk = -1;
+    if (k >= 0) {
+      const int lk = sel(cx.lab, buf)[k];
+      const int sk = cx.sib[k];
+      if (lk == l) cw = k;
+      else nk = sk;
+    }
+    k = nk;
+  }
+  const bool recv_fresh = cw >= 0 ? (sel(cx.ot, buf)[cw] == NI) : true;
+  const T rs_blank = ((bflg & F_ROOT) && recv_fresh) ? T(0) : NI;
+  cd = Best<T>{T(0), kBpNone, false};
+  cd.push(((bflg & F_HB) ? bcb : rs_blank) + p, (bflg & F_HB) ? (((uint32_t)i << 1) | 0u) : kBpRestart);
+  if (l != bl) cd.push(((bflg & F_HN) ? bcn : NI) + p, (bflg & F_HN) ? (((uint32_t)i << 1) | 1u) : kBpRestart);
+}
+
+// Small C (SQ kernels): the offers from (i0, li0) on that can have an effect
+// -- a new child scoring above the given bottom, or any re-offer of a branch
+// child (it may be evicted by its turn) -- scored and compacted into the
+// slot in offer order, up to 64, scanning 64 offers in (branch, label index)
+// order per step.  A branch whose turn is closed at that bottom (closed then:
+// closed at its turn, as the bottom only rises) ends the frame's grow before
+// it (gstop).  Any bottom at or below the true one gives a correct chunk.
+template <typename T>
+__device__ __forceinline__ void gather_small_scored(const Ctx<T>& cx, int buf, int nb, T norm, T bottom, int& i0,
+                                                    int& li0, bool& gstop, CTCX_LDS u32x4* qa, CTCX_LDS float* qp,
+                                                    int& cqn) {
+  const int lane = threadIdx.x & 63;
+  const int Cm1 = cx.C - 1, blank = cx.blank;
+  const float rcp = 1.0f / (float)Cm1;
+  cqn = 0;
+  while (cqn < 64 && i0 < nb) {
+    const int x = li0 + lane;
+    int q = (int)((float)x * rcp);
+    q -= (q * Cm1 > x) ? 1 : 0;
+    q += ((q + 1) * Cm1 <= x) ? 1 : 0;
+    const int iv = i0 + q;
+    const bool v = iv < nb;
+    const int i = v ? iv : i0;
+    const int li = v ? x - q * Cm1 : 0;
+    const int l = li + (li >= blank ? 1 : 0);
+    T s, bt;
+    int cw;
+    Best<T> cd;
+    sq_score<T>(cx, buf, norm, v, i, l, s, bt, cw, cd);
+    // a turn starting in this step (label index 0) and closed at this bottom
+    const uint64_t brkM = __ballot(v && li == 0 && !(bt > bottom));
+    const int kb = brkM ? (int)__builtin_ctzll(brkM) : 64;
+    const bool want = v && ((s > bottom) || cw >= 0) && lane < kb;
+    uint64_t wM = __ballot(want);
+    int rank = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(wM >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)wM, 0u));
+    const int room = 64 - cqn;
+    int adv;   // offers of the step passed over
+    if (__builtin_popcountll(wM) > room) {   // the chunk fills: resume after its last offer
+      wM = __ballot(want && rank < room);
+      adv = 64 - __builtin_clzll(wM);
+    } else {
+      adv = kb;
+      if (kb < 64) gstop = true;
+    }
+    if ((wM >> lane) & 1ull) {
+      u32x4 e;
+      e.x = __builtin_bit_cast(unsigned, (float)s);
+      e.y = __builtin_bit_cast(unsigned, (float)bt);
+      e.z = sq_pack(i, cw, l);
+      e.w = cd.bp;
+      qa[cqn + rank] = e;
+      qp[cqn + rank] = (float)cd.p;
+    }
+    cqn += __builtin_popcountll(wM);
+    // (i0, li0) += adv offers
+    const int xa = li0 + adv;
+    int qa2 = (int)((float)xa * rcp);
+    qa2 -= (qa2 * Cm1 > xa) ? 1 : 0;
+    qa2 += ((qa2 + 1) * Cm1 <= xa) ? 1 : 0;
+    i0 += qa2;
+    li0 = xa - qa2 * Cm1;
+    if (gstop) break;
+  }
+}
+
+// The scored gather queue's helper (SQ kernels): as help_gather_chunks, one
+// chunk ahead of wave 0 (lead 1), each chunk's offers scored (sq_score).
+template <typename T, bool BIG>
+__device__ __forceinline__ void help_gather_scored(const Ctx<T>& cx, GQ q, int buf, int nb, T norm, T pmax,
+                                                   T bottom) {
+  const int lane = threadIdx.x & 63;
+  CTCX_LDS int* m = cx.misc;
+  if (ctl_ld(m, kCtlDead) != 0) return;
+  const int blank = cx.blank;
+  const int tsn = BIG ? cx.rns : 0;
+  const T txo = BIG ? cx.rxout : ninf<T>();
+  int i0 = 0, li0 = 0, cbr = -1;
+  bool gstop = false;
+  for (int c = 0;; ++c) {
+    bool done = false;
+    uint64_t tw = 0;
+    for (int spin = 0;; ++spin) {   // the grow still running, and wave 0 at most one chunk behind
+      if (ctl_ld(m, kCtlDone) != 0) { done = true; break; }
+      if (wait_expired(spin, tw)) {
+        __hip_atomic_store(&m[kCtlDead], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        done = true;
+        break;
+      }
+      if (c <= ctl_ld(m, kCtlCons)) break;
+      __builtin_amdgcn_s_sleep(CTCX_SLEEP);
+    }
+    if (done) break;
+    // wave 0's bottom after its last chunk (it only rises)
+    const T pb = (T)__builtin_bit_cast(float, (unsigned)ctl_ld(m, kCtlBot));
+    bottom = pb > bottom ? pb : bottom;
+    const int slot = c % kQSlots;
+    const int s_i0 = i0, s_l0 = li0;
+    int cqn = 0;
+    CTCX_LDS u32x4* qa = q.a + slot * 64;
+    CTCX_LDS float* qp = q.p + slot * 64;
+    if constexpr (BIG) {
+      // the compacted (branch, label index) entries go to the slot's value
+      // array first; each lane then scores its entry and overwrites its own
+      // value word
+      CTCX_LDS uint32_t* sc = (CTCX_LDS uint32_t*)qp;
+      gather_chunk<T>(cx, buf, nb, norm, pmax, bottom, tsn, txo, i0, li0, cbr, gstop, sc, cqn, nullptr);
+      wsync<true>();
+      const bool v = lane < cqn;
+      const uint32_t e = sc[v ? lane : 0];
+      const int i = v ? (int)(e >> 16) : 0;
+      const int li = v ? (int)(e & 0xFFFFu) : 0;
+      const int l = li + (li >= blank ? 1 : 0);
+      T s, bt;
+      int cw;
+      Best<T> cd;
+      sq_score<T>(cx, buf, norm, v, i, l, s, bt, cw, cd);
+      wsync<true>();
+      if (v) {
+        u32x4 ev;
+        ev.x = __builtin_bit_cast(unsigned, (float)s);
+        ev.y = __builtin_bit_cast(unsigned, (float)bt);
+        ev.z = sq_pack(i, cw, l);
+        ev.w = cd.bp;
+        qa[lane] = ev;
+        qp[lane] = (float)cd.p;
+      }
+    } else {
+      gather_small_scored<T>(cx, buf, nb, norm, bottom, i0, li0, gstop, qa, qp, cqn);
+    }
+    if (lane == 0) {
+      q.h[slot * 4 + 0] = cqn;
+      q.h[slot * 4 + 1] = s_i0;
+      q.h[slot * 4 + 2] = s_l0;
+      q.h[slot * 4 + 3] = gstop ? 1 : 0;
+    }
+    __hip_atomic_store(&m[kCtlReady], c + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (cqn == 0 || gstop) break;   // the last chunk of the frame
+  }
+  if (BIG && cbr >= 0) cq_children(cx, buf, nb, cbr, -1);   // the child bitmap starts the next frame clear
 }
 
 template <typename T>
@@ -2049,9 +2245,12 @@ __device__ __forceinline__ void help_gather_chunks(const Ctx<T>& cx, GQ q, int b
   if (cbr >= 0) cq_children(cx, buf, nb, cbr, -1);   // the child bitmap starts the next frame clear
 }
 
-template <typename T, int RN, bool BIG, class SC, bool HW>
+template <typename T, int RN, bool BIG, class SC, bool HW, bool SQ>
 __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, bool last, int P, int* n_out,
                           int* n_leaves, uint64_t* pc, Tab tb, GQ gq) {
+  // SQ: the scored gather queue (two-wave kernels, beams <= 128, any C): with
+  // the beam full, every chunk of the grow comes from the helper scored
+  static_assert(!SQ || (HW && RN == 1), "SQ kernels");
   uint64_t ts0 = pc ? __builtin_amdgcn_s_memtime() : 0;
   // HW: both waves run up to the recursion, then wave 1 becomes the helper;
   // wave 0 (threadIdx.x == lane) runs the rest
@@ -2107,7 +2306,9 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
   if (__ballot(nonfinite)) return 1;
   if constexpr (HW) {
     if (tid >= 64) {
-      if constexpr (BIG) {
+      if constexpr (SQ) {
+        if (nb >= W) help_gather_scored<T, BIG>(cx, gq, buf, nb, norm, pmax, wave_min(lmin));
+      } else if constexpr (BIG) {
         // how far ahead of wave 0 the helper gathers (at most kQSlots chunks):
         // a chunk gathered early carries offers a later bottom rejects, and at
         // beams of <= 128 wave 0 runs those chunks faster than the helper
@@ -2176,12 +2377,14 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
   bool dz = false;           // a branch was deactivated this frame (HW window loop: bst then read)
   int gqc = 0;               // HW, large C: chunks taken from the gather queue
   uint32_t gqe = 0, gqp = 0; // ... this chunk's entry of the lane and of the lane before
+  u32x4 gqa{};               // SQ: this lane's scored offer
+  float gqv = 0.0f;          // ... its candidate value
   // |S|, the row's top set, and the largest value outside S (pre-pass; for
   // double rows |S| = 0 and the S path below is never taken)
   const int tsn = BIG ? cx.rns : 0;
   const T txo = BIG ? cx.rxout : NI;
   while (i0 < nb && !stop) {
-    if constexpr (RN == 1 && !BIG && sizeof(T) == 4 && !SC::kStateful) {
+    if constexpr (RN == 1 && !BIG && sizeof(T) == 4 && !SC::kStateful && !SQ) {
       if (st == kTopHeap && W >= 2) {
         // the windows run as one loop of their own (each window ends with the
         // grow's state in registers; the generic chunk path's loop-carried
@@ -2247,7 +2450,11 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
         int ch = (i0 * Cm1 + li0) >> 6;
         // the chunks before this one went by the generic path: their slots are free
         __hip_atomic_store(&cx.misc[kCtlCons], ch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        do {
+        // the helper gave up in an earlier frame: no table slot is used again
+        // (inside the loop tabdead only turns on in the wait below, which
+        // then ends the grow)
+        if (cx.tabdead) stop = true;
+        if (!stop) do {
           const uint64_t tc0 = pc ? __builtin_amdgcn_s_memtime() : 0;
           const bool turnw = (li0 == 0);
           const int c = ch;   // the window's first chunk (the generic chunks before it were 64 offers each)
@@ -2277,20 +2484,21 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
             // the slot reads complete with the count (one round trip): otherwise
             // the compiler sinks them below the test, a second round trip
             __asm__ volatile("" ::"v"(ta[0]), "v"(ta[1]), "v"(tpv[0]), "v"(tpv[1]));
-            if (__builtin_expect(uni(rdy) < need || cx.tabdead, 0)) {
+            if (__builtin_expect(uni(rdy) < need, 0)) {
               // wave 1 is behind (rare): wait for the count, then read again.
               // A wait that runs out of time, or a helper that gave up, ends
               // this frame's grow here and every later frame's at its first
               // window: the table's slots are never used then (the host
               // decodes the call again with the one-wave kernel, or fails it)
               uint64_t tw = 0;
-              for (int spin = 0; !cx.tabdead; ++spin) {
+              for (int spin = 0;; ++spin) {
                 spins = spin + 1;
                 __builtin_amdgcn_s_sleep(CTCX_SLEEP);
                 if (ctl_ld(cx.misc, kCtlReady) >= need) break;
                 if (ctl_ld(cx.misc, kCtlDead) != 0 || wait_expired(spin, tw)) {   // never in a correct run
                   cx.tabdead = 1;
                   __hip_atomic_store(&cx.misc[kCtlDead], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                  break;
                 }
               }
               if (cx.tabdead) {
@@ -2585,20 +2793,32 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     // checked here at the current bottom (closed now: closed at its turn, the
     // grow ends after this chunk) and again in the chunk at the bottom its turn
     // sees (sl, bat below).
-    if (BIG && full) {
+    if ((BIG || SQ) && full) {
       if constexpr (HW) {
         // the next chunk of wave 1's gather queue (the published count is read
         // first, so the reads issued after it see the chunk)
         const int slot = gqc % kQSlots;
         int h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+        auto read_slot = [&]() {
+          h0 = gq.h[slot * 4 + 0]; h1 = gq.h[slot * 4 + 1]; h2 = gq.h[slot * 4 + 2]; h3 = gq.h[slot * 4 + 3];
+          if constexpr (SQ) {
+            gqa = gq.a[slot * 64 + lane];
+            gqv = gq.p[slot * 64 + lane];
+            gqp = gq.a[slot * 64 + (lane > 0 ? lane - 1 : 0)].z;
+          } else {
+            gqe = gq.e[slot * 64 + lane];
+            gqp = gq.e[slot * 64 + (lane > 0 ? lane - 1 : 0)];
+          }
+        };
         {
           // one batch of reads, no loop around it (see the score-table read)
           const int rdy = __hip_atomic_load(&cx.misc[kCtlReady], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           __asm__ volatile("" ::: "memory");
-          h0 = gq.h[slot * 4 + 0]; h1 = gq.h[slot * 4 + 1]; h2 = gq.h[slot * 4 + 2]; h3 = gq.h[slot * 4 + 3];
-          gqe = gq.e[slot * 64 + lane];
-          gqp = gq.e[slot * 64 + (lane > 0 ? lane - 1 : 0)];
-          __asm__ volatile("" ::"v"(h0), "v"(h1), "v"(h2), "v"(h3), "v"(gqe), "v"(gqp));   // one round trip
+          read_slot();
+          if constexpr (SQ)
+            __asm__ volatile("" ::"v"(h0), "v"(h1), "v"(h2), "v"(h3), "v"(gqa), "v"(gqv), "v"(gqp));   // one round trip
+          else
+            __asm__ volatile("" ::"v"(h0), "v"(h1), "v"(h2), "v"(h3), "v"(gqe), "v"(gqp));
           if (__builtin_expect(uni(rdy) <= gqc && !cx.tabdead, 0)) {
             // wave 1 is behind: wait for the count, then read again (a wait that
             // runs out of time, or a helper that gave up, takes cqn = 0 below:
@@ -2615,9 +2835,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
               }
             }
             __asm__ volatile("" ::: "memory");
-            h0 = gq.h[slot * 4 + 0]; h1 = gq.h[slot * 4 + 1]; h2 = gq.h[slot * 4 + 2]; h3 = gq.h[slot * 4 + 3];
-            gqe = gq.e[slot * 64 + lane];
-            gqp = gq.e[slot * 64 + (lane > 0 ? lane - 1 : 0)];
+            read_slot();
           }
         }
         __asm__ volatile("" ::: "memory");
@@ -2640,98 +2858,134 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     // small C: the turn check of a branch starting at this chunk's lane 0 uses
     // that lane's total from the chunk's read batch below (a branch spans few
     // chunks, and the chunk test below suffices for the rest)
-    const bool turn0 = !BIG && full && li0 == 0;
+    const bool turn0 = !BIG && !SQ && full && li0 == 0;
     const uint64_t tc0 = pc ? __builtin_amdgcn_s_memtime() : 0;
-    bool valid;
-    int i, li, sl;   // sl: the lane where this lane's branch turn starts in the chunk (see bat below)
-    if (BIG && full) {
-      // the compacted chunk: lane j < cqn holds the j-th gathered offer; a
-      // branch turn starts at the first lane of its branch unless the branch
-      // began before the span
+    // the chunk's lanes: offer (branch i, label l), valid / live, score s, the
+    // branch total bt, the branch child c it re-offers (-1: none) and whether
+    // that child has been evicted (cev), the child's label-ending candidate cd
+    bool valid, live, isbc, cev;
+    int i, l, c;
+    int sl;   // the lane where this lane's branch turn starts in the chunk (see bat below)
+    T s, bt;
+    T cst = T(0);   // the child's scorer state (ExpandState, decoder.h:171)
+    Best<T> cd{T(0), kBpNone, false};
+    if (SQ && full) {
+      // a scored chunk (help_gather_scored): lane j < cqn holds the j-th
+      // gathered offer ready to push; what events change is read here: the
+      // branch deactivated (only after a deactivation this frame), the branch
+      // child evicted (only when a lane re-offers one)
       valid = lane < cqn;
-      uint32_t e, ep;
-      if constexpr (HW) {
-        e = valid ? gqe : (uint32_t)__builtin_amdgcn_readfirstlane(gqe);   // (read with the slot's header)
-        ep = gqp;
-      } else {
-        CTCX_LDS uint32_t* cq = row_cq(cx);
-        e = cq[valid ? lane : 0];
-        ep = cq[lane > 0 ? lane - 1 : 0];
-      }
-      i = (int)(e >> 16);
-      li = (int)(e & 0xFFFFu);
-      const int ip = lane > 0 ? (int)(ep >> 16) : -1;
+      const uint32_t pk = valid ? gqa.z : 0u;   // (lanes past cqn: branch 0, no child)
+      i = (int)(pk & 255u);
+      c = (int)((pk >> 8) & 255u) - 1;
+      l = (int)(pk >> 16);
+      s = (T)__builtin_bit_cast(float, gqa.x);
+      bt = (T)__builtin_bit_cast(float, gqa.y);
+      cd = Best<T>{(T)gqv, gqa.w, true};
+      const int ip = lane > 0 ? (int)(gqp & 255u) : -1;
       const uint64_t fm = __ballot(valid && i != ip) & lowmask(lane + 1);
       sl = (i > cq_i0 || cq_l0 == 0) ? 63 - __builtin_clzll(fm) : -1;
+      isbc = c >= 0;
+      live = valid;
+      if (dz) live = live && !(cx.bst[i] & S_DEACT);
+      cev = false;
+      if (__ballot(isbc)) cev = isbc && (cx.bst[isbc ? c : i] & S_EVICT);
     } else {
-      // lane -> (branch, label index): x / Cm1 for x < 64 + Cm1, by float reciprocal
-      const int x = li0 + lane;
-      int q = (int)((float)x * rcp);
-      q -= (q * Cm1 > x) ? 1 : 0;
-      q += ((q + 1) * Cm1 <= x) ? 1 : 0;
-      const int iv = i0 + q;
-      valid = iv < nb;
-      i = valid ? iv : i0;
-      li = valid ? x - q * Cm1 : 0;
-      for (li0 += 64; li0 >= Cm1; li0 -= Cm1) ++i0;
-      sl = lane - li;
+      int li;
+      if (BIG && full) {
+        // the compacted chunk: lane j < cqn holds the j-th gathered offer; a
+        // branch turn starts at the first lane of its branch unless the branch
+        // began before the span
+        valid = lane < cqn;
+        uint32_t e, ep;
+        if constexpr (HW) {
+          e = valid ? gqe : (uint32_t)__builtin_amdgcn_readfirstlane(gqe);   // (read with the slot's header)
+          ep = gqp;
+        } else {
+          CTCX_LDS uint32_t* cq = row_cq(cx);
+          e = cq[valid ? lane : 0];
+          ep = cq[lane > 0 ? lane - 1 : 0];
+        }
+        i = (int)(e >> 16);
+        li = (int)(e & 0xFFFFu);
+        const int ip = lane > 0 ? (int)(ep >> 16) : -1;
+        const uint64_t fm = __ballot(valid && i != ip) & lowmask(lane + 1);
+        sl = (i > cq_i0 || cq_l0 == 0) ? 63 - __builtin_clzll(fm) : -1;
+      } else {
+        // lane -> (branch, label index): x / Cm1 for x < 64 + Cm1, by float reciprocal
+        const int x = li0 + lane;
+        int q = (int)((float)x * rcp);
+        q -= (q * Cm1 > x) ? 1 : 0;
+        q += ((q + 1) * Cm1 <= x) ? 1 : 0;
+        const int iv = i0 + q;
+        valid = iv < nb;
+        i = valid ? iv : i0;
+        li = valid ? x - q * Cm1 : 0;
+        for (li0 += 64; li0 >= Cm1; li0 -= Cm1) ++i0;
+        sl = lane - li;
+      }
+      l = li + (li >= blank ? 1 : 0);
+      // one batch of LDS reads, every lane (i is a valid branch, l a valid
+      // label), so the chunk waits on LDS once before its skip test
+      const int bl = sel(cx.lab, buf)[i];
+      const int bflg = sel(cx.flg, buf)[i];
+      bt = sel(cx.ot, buf)[i];
+      const T bob = sel(cx.ob, buf)[i];
+      const int bsti = cx.bst[i];
+      const uint64_t blm = cx.bloom[i];
+      const int hd = cx.head[i];
+      const T bcb = sel(cx.cb, buf)[i], bcn = sel(cx.cn, buf)[i];
+      const T xl = cx.row[l];
+      if (turn0 && !(bcast(bt, 0) > bottom)) break;   // branch i0's turn: skipped, and all later
+      live = valid && !(bsti & S_DEACT);
+      const T p = xl - norm;
+      T base = (l == bl) ? bob : bt;
+      if constexpr (SC::kStateful) {
+        cst = SC::expand(cx, sel(cx.est, buf)[i], bl, l);
+        base = SC::score(cst, base);
+      }
+      s = p + base;
+      // the skip test below with the evicted-children bloom in place of the
+      // children (found after it)
+      if (full && !__ballot(live && ((s > bottom) | (((blm >> (l & 63)) & 1ull) != 0)))) {
+        if (__ballot(valid && sl == lane && lane != 0) & ~__ballot(bt > bottom)) break;   // no event here: every start sees this bottom
+        if (gstop) break;
+        continue;
+      }
+      // the branch child this offer re-offers, if any (GetChild finds it): walk
+      // branch i's children, each step one read pair (label, next sibling)
+      c = -1;
+      for (int k = live ? hd : -1; __ballot(k >= 0);) {
+        int nk = -1;
+        if (k >= 0) {
+          const int lk = sel(cx.lab, buf)[k];
+          const int sk = cx.sib[k];
+          if (lk == l) c = k;
+          else nk = sk;
+        }
+        k = nk;
+      }
+      isbc = c >= 0;
+      const int cc = isbc ? c : i;
+      cev = isbc && (cx.bst[cc] & S_EVICT);
+      // label-ending candidate for the child (decoder.h:172-185), from branch i's
+      // candidates read in the batch above
+      const bool recv_fresh = isbc ? (sel(cx.ot, buf)[cc] == NI) : true;
+      const T rs_blank = ((bflg & F_ROOT) && recv_fresh) ? T(0) : NI;
+      cd.push(((bflg & F_HB) ? bcb : rs_blank) + p, (bflg & F_HB) ? (((uint32_t)i << 1) | 0u) : kBpRestart);
+      if (l != bl) cd.push(((bflg & F_HN) ? bcn : NI) + p, (bflg & F_HN) ? (((uint32_t)i << 1) | 1u) : kBpRestart);
     }
-    const int l = li + (li >= blank ? 1 : 0);
-    // one batch of LDS reads, every lane (i is a valid branch, l a valid
-    // label), so the chunk waits on LDS once before its skip test
-    const int bl = sel(cx.lab, buf)[i];
-    const int bflg = sel(cx.flg, buf)[i];
-    const T bt = sel(cx.ot, buf)[i];
-    const T bob = sel(cx.ob, buf)[i];
-    const int bsti = cx.bst[i];
-    const uint64_t blm = cx.bloom[i];
-    const int hd = cx.head[i];
-    const T bcb = sel(cx.cb, buf)[i], bcn = sel(cx.cn, buf)[i];
-    const T xl = cx.row[l];
-    if (turn0 && !(bcast(bt, 0) > bottom)) break;   // branch i0's turn: skipped, and all later
-    bool live = valid && !(bsti & S_DEACT);
-    const T p = xl - norm;
-    T base = (l == bl) ? bob : bt;
-    T cst = T(0);   // the child's scorer state (ExpandState, decoder.h:171)
-    if constexpr (SC::kStateful) {
-      cst = SC::expand(cx, sel(cx.est, buf)[i], bl, l);
-      base = SC::score(cst, base);
-    }
-    const T s = p + base;
     // sl: the lane where this lane's branch turn starts in the chunk (< 0: in
     // an earlier chunk, found open there), and the bottom at that moment (bat:
     // refreshed after every event for turns that start later in the chunk)
     T bat = sl > 0 ? bottom : NI;
     const uint64_t startsM = __ballot(valid && sl == lane && lane != 0);   // branch turns starting mid-chunk
     if (pc) pc[10] += __builtin_amdgcn_s_memtime() - tc0;
-    if (full && !__ballot(live && ((s > bottom) | (((blm >> (l & 63)) & 1ull) != 0)))) {
+    if (SQ && full && !__ballot(live && ((s > bottom) | (isbc && cev)))) {
       if (startsM & ~__ballot(bt > bottom)) break;   // no event here: every start sees this bottom
       if (gstop) break;
       continue;
     }
-    // the branch child this offer re-offers, if any (GetChild finds it): walk
-    // branch i's children, each step one read pair (label, next sibling)
-    int c = -1;
-    for (int k = live ? hd : -1; __ballot(k >= 0);) {
-      int nk = -1;
-      if (k >= 0) {
-        const int lk = sel(cx.lab, buf)[k];
-        const int sk = cx.sib[k];
-        if (lk == l) c = k;
-        else nk = sk;
-      }
-      k = nk;
-    }
-    const bool isbc = c >= 0;
-    const int cc = isbc ? c : i;
-    bool cev = isbc && (cx.bst[cc] & S_EVICT);
-    // label-ending candidate for the child (decoder.h:172-185), from branch i's
-    // candidates read in the batch above
-    const bool recv_fresh = isbc ? (sel(cx.ot, buf)[cc] == NI) : true;
-    const T rs_blank = ((bflg & F_ROOT) && recv_fresh) ? T(0) : NI;
-    Best<T> cd{T(0), kBpNone, false};
-    cd.push(((bflg & F_HB) ? bcb : rs_blank) + p, (bflg & F_HB) ? (((uint32_t)i << 1) | 0u) : kBpRestart);
-    if (l != bl) cd.push(((bflg & F_HN) ? bcn : NI) + p, (bflg & F_HN) ? (((uint32_t)i << 1) | 1u) : kBpRestart);
     const uint64_t isbm = __ballot(isbc);
 
     uint64_t tc1 = pc ? __builtin_amdgcn_s_memtime() : 0;
@@ -3041,7 +3295,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       }
     }
     // the turn continuing into the next chunk: skipped -> so is every later one
-    if (full && (__ballot(valid && !(bt > bat)) >> ((BIG && full) ? cqn - 1 : 63)) & 1ull) stop = true;
+    if (full && (__ballot(valid && !(bt > bat)) >> (((BIG || SQ) && full) ? cqn - 1 : 63)) & 1ull) stop = true;
     if (gstop) stop = true;
     // flush: resets and flags first, then the surviving accepted entries
     const uint64_t q5 = pc ? __builtin_amdgcn_s_memtime() : 0;
@@ -3052,10 +3306,12 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       } else {
         cx.et[rs] = NI; cx.eb[rs] = NI; cx.el[rs] = NI; cx.eflg[rs] = 0;
         __hip_atomic_fetch_or(&cx.bst[rs], S_EVICT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const int par = sel(cx.par, buf)[rs];
-        if (par >= 0)
-          __hip_atomic_fetch_or(&cx.bloom[par], 1ull << (sel(cx.lab, buf)[rs] & 63), __ATOMIC_RELAXED,
-                                __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (!(SQ && full)) {   // (scored chunks know their branch children: no bloom)
+          const int par = sel(cx.par, buf)[rs];
+          if (par >= 0)
+            __hip_atomic_fetch_or(&cx.bloom[par], 1ull << (sel(cx.lab, buf)[rs] & 63), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
       }
     }
     if (myslot >= 0) {
@@ -3067,7 +3323,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       if constexpr (SC::kStateful) cx.eest[myslot] = cst;
       if (isbc) __hip_atomic_fetch_and(&cx.bst[c], ~S_EVICT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    if constexpr (HW && BIG)   // the helper gathers the next chunks against this bottom
+    if constexpr (HW && (BIG || SQ))   // the helper gathers the next chunks against this bottom
       if (full)
         __hip_atomic_store(&cx.misc[kCtlBot], (int)__builtin_bit_cast(unsigned, (float)bottom), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -3776,9 +4032,10 @@ __device__ void ring_flush(const Ring<RT>& g, RT* out, int32_t* foff, int t_new,
 // HW: two waves per item (wave 1 the helper, see help_score_chunks); every
 // loop over positions below then runs over NT = 128 threads, and one-thread
 // work is thread 0's (wave 0, the decoding wave).
-template <typename T, int RN, int WC, bool BIG, class SC, bool HW>
+template <typename T, int RN, int WC, bool BIG, class SC, bool HW, bool SQ = false>
 __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T> prm) {
   static_assert(!HW || (sizeof(T) == 4 && !SC::kStateful && (BIG ? WC > 0 : (RN == 1 && WC == 128))), "HW kernels");
+  static_assert(!SQ || (HW && RN == 1 && WC == 128), "SQ kernels");
   constexpr int NT = HW ? 128 : 64;
   Ctx<T> cx;
 #ifdef CTCX_GSTATE
@@ -3818,13 +4075,13 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
 #ifndef CTCX_GSTATE
   {
     size_t off = (decode_lds_bytes(WC > 0 ? WC : W, C, (int)sizeof(T), SC::kStateful) + 15) & ~(size_t)15;
-    if constexpr (HW && !BIG) {
+    if constexpr (HW && !BIG && !SQ) {
       tb = tab_carve((CTCX_LDS char*)lds + off);
       off += tab_lds_bytes();
     }
-    if constexpr (HW && BIG) {
-      gq = gq_carve((CTCX_LDS char*)lds + off);
-      off += gq_lds_bytes();
+    if constexpr (HW && (BIG || SQ)) {
+      gq = gq_carve<SQ>((CTCX_LDS char*)lds + off);
+      off += gq_lds_bytes(SQ);
     }
     if (R > 0) rg = ring_carve<RT>((CTCX_LDS char*)lds + off, R, W);
   }
@@ -3942,7 +4199,7 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
     if (prof) pc[0] += t1 - t0;
 #ifndef CTCX_GSTATE   // the global-state tier replays every frame literally
     if (!prm.force_literal && !dup)
-      why = exact_step<T, RN, BIG, SC, HW>(cx, buf, nb, norm, last, prm.P, &n, &nl_fast, prof ? pc : nullptr, tb, gq);
+      why = exact_step<T, RN, BIG, SC, HW, SQ>(cx, buf, nb, norm, last, prm.P, &n, &nl_fast, prof ? pc : nullptr, tb, gq);
 #endif
     if constexpr (HW) {
       // wave 0's result for both waves; the helper stops if the grow ended
@@ -4980,19 +5237,21 @@ __global__ __launch_bounds__(64) void ctcx_pack(PackParams pp) {
 // Launchers (called by the C-ABI layer).
 namespace ctcx {
 
-template <typename T, int RN, int WC, bool BIG, class SC, bool HW = false>
+template <typename T, int RN, int WC, bool BIG, class SC, bool HW = false, bool SQ = false>
 hipError_t launch_decode_c(const DecodeParams<T>& p, hipStream_t s) {
-  // the decode layout, then (HW) the score table, then the record ring
+  // the decode layout, then (HW) the score table or gather queue, then the
+  // record ring (its size by the same functions as the host's checks)
   size_t lds = decode_lds_bytes(WC > 0 ? WC : p.W, p.C, (int)sizeof(T), SC::kStateful);
-  if (HW) lds = ((lds + 15) & ~(size_t)15) + (BIG ? gq_lds_bytes() : tab_lds_bytes());
+  if (HW) lds = ((lds + 15) & ~(size_t)15) + ((BIG || SQ) ? gq_lds_bytes(SQ) : tab_lds_bytes());
   if (p.ring > 0) lds = ((lds + 15) & ~(size_t)15) + ring_lds_bytes(p.ring, p.W, HW && !BIG ? 4 : 8);
+  if (lds > kLdsBytes) return hipErrorInvalidValue;
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)ctcx_beam_decode<T, RN, WC, BIG, SC, HW>,
+    hipError_t e = hipFuncSetAttribute((const void*)ctcx_beam_decode<T, RN, WC, BIG, SC, HW, SQ>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((ctcx_beam_decode<T, RN, WC, BIG, SC, HW>), dim3((unsigned)p.B), dim3(HW ? 128 : 64), lds, s,
-                     p);
+  hipLaunchKernelGGL((ctcx_beam_decode<T, RN, WC, BIG, SC, HW, SQ>), dim3((unsigned)p.B), dim3(HW ? 128 : 64), lds,
+                     s, p);
   return hipGetLastError();
 }
 
@@ -5038,6 +5297,8 @@ hipError_t launch_decode_c(const DecodeParams<T>& p, hipStream_t s) {
 #define CTCX_IF_7(...)
 #define CTCX_IF_8(...)
 #define CTCX_IF_10(...)
+#define CTCX_IF_11(...)
+#define CTCX_IF_12(...)
 #if CTCX_PART == 1
 #undef CTCX_IF_1
 #define CTCX_IF_1(...) __VA_ARGS__
@@ -5065,6 +5326,12 @@ hipError_t launch_decode_c(const DecodeParams<T>& p, hipStream_t s) {
 #elif CTCX_PART == 10
 #undef CTCX_IF_10
 #define CTCX_IF_10(...) __VA_ARGS__
+#elif CTCX_PART == 11
+#undef CTCX_IF_11
+#define CTCX_IF_11(...) __VA_ARGS__
+#elif CTCX_PART == 12
+#undef CTCX_IF_12
+#define CTCX_IF_12(...) __VA_ARGS__
 #endif
 #define CTCX_IF_PART(P, ...) CTCX_IF_##P(__VA_ARGS__)
 #if CTCX_PART == 0
@@ -5084,12 +5351,21 @@ extern template hipError_t launch_decode_c<float, 1, 128, true, BaseBeamScorer<f
     const DecodeParams<float>&, hipStream_t);
 extern template hipError_t launch_decode_c<float, 2, 256, true, BaseBeamScorer<float>, true>(
     const DecodeParams<float>&, hipStream_t);
+extern template hipError_t launch_decode_c<float, 1, 128, false, BaseBeamScorer<float>, true, true>(
+    const DecodeParams<float>&, hipStream_t);
+extern template hipError_t launch_decode_c<float, 1, 128, true, BaseBeamScorer<float>, true, true>(
+    const DecodeParams<float>&, hipStream_t);
 #else
 CTCX_IF_PART(8, template hipError_t launch_decode_c<float, 1, 128, false, BaseBeamScorer<float>, true>(
                     const DecodeParams<float>&, hipStream_t);)
 CTCX_IF_PART(10, template hipError_t launch_decode_c<float, 1, 128, true, BaseBeamScorer<float>, true>(
                      const DecodeParams<float>&, hipStream_t);)
 CTCX_IF_PART(10, template hipError_t launch_decode_c<float, 2, 256, true, BaseBeamScorer<float>, true>(
+                     const DecodeParams<float>&, hipStream_t);)
+// the scored gather queue (beams <= 128): small C (part 11), large C (part 12)
+CTCX_IF_PART(11, template hipError_t launch_decode_c<float, 1, 128, false, BaseBeamScorer<float>, true, true>(
+                     const DecodeParams<float>&, hipStream_t);)
+CTCX_IF_PART(12, template hipError_t launch_decode_c<float, 1, 128, true, BaseBeamScorer<float>, true, true>(
                      const DecodeParams<float>&, hipStream_t);)
 #endif
 
@@ -5104,12 +5380,15 @@ static hipError_t launch_decode_r(const DecodeParams<T>& p, hipStream_t s) {
 
 // The two-wave kernel a shape can run (helper_kind; 0: none): 1 the score
 // table (float, beams <= 128, C <= 64; 4-byte records), 2 the gather queue
-// (float, beams <= 256, C > 64).  The base scorer only.  The host decides once
-// per call (enqueue_shard), with CTCEXT_HELPER=0 (diagnostics) or the
-// one-wave re-decode after a helper timeout choosing none.
+// (float, beams <= 256, C > 64), 3 the scored gather queue (float, beams <=
+// 128, any C; 4-byte records for C <= 64).  The base scorer only.  mode (the
+// host's, once per call in enqueue_shard): kHelperNone (CTCEXT_HELPER=0, or
+// the one-wave re-decode after a helper timeout), kHelperLegacy (kinds 1 and
+// 2 only), kHelperScored (kind 3 where it applies).
 template <typename T>
-int helper_kind(const DecodeParams<T>& p) {
-  if (sizeof(T) != 4 || p.scorer_tab != nullptr) return 0;
+int helper_kind(const DecodeParams<T>& p, int mode) {
+  if (mode == kHelperNone || sizeof(T) != 4 || p.scorer_tab != nullptr) return 0;
+  if (mode == kHelperScored && p.W <= 128) return 3;
   if (p.C <= kRec32MaxClasses) return p.W <= kRec32MaxBeam ? 1 : 0;
   return p.W <= 256 ? 2 : 0;
 }
@@ -5119,7 +5398,7 @@ __host__ inline int helper_wc(int W) { return W <= 128 ? 128 : 256; }
 template <typename T>
 size_t pre_ring_lds_bytes(const DecodeParams<T>& p, int hk, int wc) {
   const size_t b = (decode_lds_bytes(wc, p.C, (int)sizeof(T), p.scorer_tab != nullptr) + 15) & ~(size_t)15;
-  return hk == 1 ? b + tab_lds_bytes() : hk == 2 ? b + gq_lds_bytes() : b;
+  return hk == 1 ? b + tab_lds_bytes() : hk == 2 ? b + gq_lds_bytes(false) : hk == 3 ? b + gq_lds_bytes(true) : b;
 }
 // the two-wave kernel this call runs (0: none), given the kind the host chose
 // (hk): its layout and ring must fit
@@ -5127,13 +5406,13 @@ template <typename T>
 int use_helper_kernel(const DecodeParams<T>& p, int hk) {
   if (hk == 0) return 0;
   size_t b = pre_ring_lds_bytes(p, hk, helper_wc(p.W));
-  if (p.ring > 0) b = ((b + 15) & ~(size_t)15) + ring_lds_bytes(p.ring, p.W, hk == 1 ? 4 : 8);
+  if (p.ring > 0) b = ((b + 15) & ~(size_t)15) + ring_lds_bytes(p.ring, p.W, helper_rec32(hk, p.C) ? 4 : 8);
   return b <= kLdsBytes ? hk : 0;
 }
 template int use_helper_kernel<float>(const DecodeParams<float>&, int);
 template int use_helper_kernel<double>(const DecodeParams<double>&, int);
-template int helper_kind<float>(const DecodeParams<float>&);
-template int helper_kind<double>(const DecodeParams<double>&);
+template int helper_kind<float>(const DecodeParams<float>&, int);
+template int helper_kind<double>(const DecodeParams<double>&, int);
 
 template <typename T>
 hipError_t launch_decode(const DecodeParams<T>& p, hipStream_t s) {
@@ -5156,6 +5435,9 @@ hipError_t launch_decode(const DecodeParams<T>& p, hipStream_t s) {
     if (hk == 2)
       return p.W <= 128 ? launch_decode_c<float, 1, 128, true, BaseBeamScorer<float>, true>(p, s)
                         : launch_decode_c<float, 2, 256, true, BaseBeamScorer<float>, true>(p, s);
+    if (hk == 3)
+      return p.C > 64 ? launch_decode_c<float, 1, 128, true, BaseBeamScorer<float>, true, true>(p, s)
+                      : launch_decode_c<float, 1, 128, false, BaseBeamScorer<float>, true, true>(p, s);
   }
   if (p.W <= 128) return fits(128) ? launch_decode_r<T, 1, 128>(p, s) : launch_decode_r<T, 1, 0>(p, s);
   if (p.W <= 256) return fits(256) ? launch_decode_r<T, 2, 256>(p, s) : launch_decode_r<T, 2, 0>(p, s);
@@ -5178,8 +5460,10 @@ int ring_frames(const DecodeParams<T>& p, int cus, int cap, int hk) {
   if ((int64_t)p.Tmax * p.W > 0x7fffffffLL) return 0;
   // the two-wave kernel the host chose (hk), when its layout and a ring fit
   // (the score table's records are 4 bytes)
-  if (hk && pre_ring_lds_bytes(p, hk, helper_wc(p.W)) + ring_lds_bytes(8, p.W, hk == 1 ? 4 : 8) > kLdsBytes) hk = 0;
-  const int rb = hk == 1 ? 4 : 8;
+  if (hk && pre_ring_lds_bytes(p, hk, helper_wc(p.W)) + ring_lds_bytes(8, p.W, helper_rec32(hk, p.C) ? 4 : 8) >
+                kLdsBytes)
+    hk = 0;
+  const int rb = helper_rec32(hk, p.C) ? 4 : 8;
   const size_t base = pre_ring_lds_bytes(p, hk, hk ? helper_wc(p.W) : wcap);
   const size_t budget = (base > 80 * 1024 || p.B <= cus) ? kLdsBytes : 80 * 1024;
   // the kernel addresses ring rows by t & (R - 1): R must be a power of two

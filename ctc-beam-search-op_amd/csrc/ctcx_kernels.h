@@ -152,6 +152,10 @@ struct DecodeParams {
   int32_t test_flags;       // kTestHelperDead: the helper wave starts out "timed out" (tests only)
 };
 constexpr int32_t kTestHelperDead = 1;
+// helper_kind's modes and the record size of a two-wave kernel kind (4-byte
+// Rec32 records: the score table, and the scored queue at C <= 64)
+constexpr int kHelperNone = 0, kHelperLegacy = 1, kHelperScored = 3;
+__host__ __device__ inline bool helper_rec32(int hk, int64_t C) { return hk == 1 || (hk == 3 && C <= kRec32MaxClasses); }
 
 struct TraceParams {
   const Rec* rec;
