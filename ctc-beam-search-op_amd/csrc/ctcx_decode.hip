@@ -2156,6 +2156,9 @@ __device__ __forceinline__ void help_gather_scored(const Ctx<T>& cx, GQ q, int b
     // wave 0's bottom after its last chunk (it only rises)
     const T pb = (T)__builtin_bit_cast(float, (unsigned)ctl_ld(m, kCtlBot));
     bottom = pb > bottom ? pb : bottom;
+#ifdef CTCX_SQ_NOFILTER   // (diagnostics: every offer gathered, no closed turn found here)
+    bottom = ninf<T>();
+#endif
     const int slot = c % kQSlots;
     const int s_i0 = i0, s_l0 = li0;
     int cqn = 0;
@@ -2245,6 +2248,9 @@ __device__ __forceinline__ void help_gather_chunks(const Ctx<T>& cx, GQ q, int b
   if (cbr >= 0) cq_children(cx, buf, nb, cbr, -1);   // the child bitmap starts the next frame clear
 }
 
+#ifdef CTCX_SQ_CHECK
+__shared__ int g_sq_dbg[8];   // (diagnostics: the first scored-field mismatch)
+#endif
 template <typename T, int RN, bool BIG, class SC, bool HW, bool SQ>
 __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, bool last, int P, int* n_out,
                           int* n_leaves, uint64_t* pc, Tab tb, GQ gq) {
@@ -2885,6 +2891,41 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       const int ip = lane > 0 ? (int)(gqp & 255u) : -1;
       const uint64_t fm = __ballot(valid && i != ip) & lowmask(lane + 1);
       sl = (i > cq_i0 || cq_l0 == 0) ? 63 - __builtin_clzll(fm) : -1;
+#ifdef CTCX_SQ_CHECK   // (diagnostics: wave 0 recomputes every scored field; mismatches counted in misc[15])
+      {
+        T s2, bt2;
+        int c2;
+        Best<T> cd2;
+        sq_score<T>(cx, buf, norm, valid, i, l, s2, bt2, c2, cd2);
+        const int fmask = (__builtin_bit_cast(unsigned, (float)s2) != __builtin_bit_cast(unsigned, (float)s) ? 1 : 0) |
+                          (__builtin_bit_cast(unsigned, (float)bt2) != __builtin_bit_cast(unsigned, (float)bt) ? 2 : 0) |
+                          (c2 != c ? 4 : 0) |
+                          (__builtin_bit_cast(unsigned, (float)cd2.p) != __builtin_bit_cast(unsigned, (float)cd.p) ? 8 : 0) |
+                          (cd2.bp != cd.bp ? 16 : 0);
+        const bool bad = valid && fmask != 0;
+        const uint64_t badM = __ballot(bad);
+        if (badM) {
+          const int kf = (int)__builtin_ctzll(badM);
+          if (lane == kf) {
+            if (__hip_atomic_fetch_add(&cx.misc[15], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
+              // the first mismatch: fields, (lane, chunk, cqn, i, l), the two scores
+              g_sq_dbg[0] = fmask | ((c + 1) << 8) | ((c2 + 1) << 16);
+              g_sq_dbg[1] = lane | (gqc << 8) | (cqn << 16);
+              g_sq_dbg[2] = i | (l << 16);
+              // the branch totals: the slot's (read with the chunk), wave 0's, and the slot's read again now
+              g_sq_dbg[3] = (int)__builtin_bit_cast(unsigned, (float)bt);
+              g_sq_dbg[4] = (int)__builtin_bit_cast(unsigned, (float)bt2);
+              g_sq_dbg[6] = (int)gq.a[((gqc - 1) % kQSlots) * 64 + lane].y;
+              g_sq_dbg[7] = (int)__builtin_bit_cast(unsigned, (float)sel(cx.ot, buf ^ 1)[i]);
+              g_sq_dbg[5] = (c & 0xffff) | (c2 << 16);
+            }
+          }
+          __hip_atomic_fetch_add(&cx.misc[15], __builtin_popcountll(badM) - 1, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        s = s2; bt = bt2; c = c2; cd = cd2;
+      }
+#endif
       isbc = c >= 0;
       live = valid;
       if (dz) live = live && !(cx.bst[i] & S_DEACT);
@@ -4101,6 +4142,7 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
     // (tests: kTestHelperDead starts the helper out as if its first wait had
     // run out of time, so the failure path runs without a hang)
     cx.misc[kCtlDead] = (HW && (prm.test_flags & kTestHelperDead)) ? 1 : 0;
+    cx.misc[15] = 0;
     cx.lab[0][0] = -1; cx.par[0][0] = -1; cx.flg[0][0] = F_ROOT;
     cx.ot[0][0] = T(0); cx.ob[0][0] = T(0); cx.ol[0][0] = ninf<T>();
     cx.cb[0][0] = T(0); cx.cn[0][0] = T(0);
@@ -4466,6 +4508,21 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
     io.why_nonfinite = why_nf;
     io.why_fill = why_fill;
     io.records = R > 0 ? (int64_t)nrec : nrec_all;
+#ifdef CTCX_SQ_CHECK
+    io.dup_frames = cx.misc[15];
+    io.why_nonfinite = g_sq_dbg[0];
+    io.why_fill = g_sq_dbg[1];
+    io.records = ((int64_t)(uint32_t)g_sq_dbg[2] << 32) | (uint32_t)g_sq_dbg[3];
+    io.literal_steps = g_sq_dbg[4];
+    io.n_leaves = n_leaves;
+    io.why_nonfinite = (io.why_nonfinite & 0xffffff) | 0;
+    io.dup_frames = g_sq_dbg[6];
+    io.pad = 0;
+    io.why_fill = (io.why_fill & 0xffffff);
+    io.records = (io.records & ~0xffffffffll) | (uint32_t)g_sq_dbg[3];
+    io.n_leaves = n_leaves;
+    prm.log_prob[b * prm.P] = (T)__builtin_bit_cast(float, (unsigned)g_sq_dbg[7]);
+#endif
     // HW kernels: a hand-over wait that gave up (the host fails the call)
     io.pad = HW ? __hip_atomic_load(&cx.misc[kCtlDead], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0;
     prm.item[b] = io;
