@@ -1611,6 +1611,13 @@ constexpr int kGatherWin = 8;   // kept 64-label windows per batch of row reads 
 // A barrier for code only wave 0 runs in HW kernels (one wave: its LDS
 // operations execute in order, so a compiler fence is enough), else the
 // workgroup barrier.
+// Two-wave kernels: which wave this is, as a wave-UNIFORM value (the
+// compiler cannot know that threadIdx.x >= 64 is uniform per wave).  Every
+// split between the decoding wave and the helper goes through it: a branch on
+// threadIdx.x is compiled as divergent control flow (both sides in one
+// sequence under exec masks); a uniform branch gives each wave its own scalar
+// path (cfg3 decode 149.4 -> 147.3 ms with the score table, same box).
+__device__ __forceinline__ bool helper_wave() { return __builtin_amdgcn_readfirstlane((int)threadIdx.x) >= 64; }
 template <bool HW>
 __device__ __forceinline__ void wsync() {
   if constexpr (HW) {
@@ -2311,7 +2318,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
   }
   if (__ballot(nonfinite)) return 1;
   if constexpr (HW) {
-    if (tid >= 64) {
+    if (helper_wave()) {
       if constexpr (SQ) {
         if (nb >= W) help_gather_scored<T, BIG>(cx, gq, buf, nb, norm, pmax, wave_min(lmin));
       } else if constexpr (BIG) {
@@ -2881,13 +2888,18 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       // branch deactivated (only after a deactivation this frame), the branch
       // child evicted (only when a lane re-offers one)
       valid = lane < cqn;
-      const uint32_t pk = valid ? gqa.z : 0u;   // (lanes past cqn: branch 0, no child)
+      // (the words go through scalar copies: clang's __builtin_bit_cast of an
+      // ext_vector element lvalue reads element 0 whatever the element -- the
+      // cause of round 4's failed scored queue, where every field read the
+      // score)
+      const uint32_t ax = gqa.x, ay = gqa.y, az = gqa.z, aw = gqa.w;
+      const uint32_t pk = valid ? az : 0u;   // (lanes past cqn: branch 0, no child)
       i = (int)(pk & 255u);
       c = (int)((pk >> 8) & 255u) - 1;
       l = (int)(pk >> 16);
-      s = (T)__builtin_bit_cast(float, gqa.x);
-      bt = (T)__builtin_bit_cast(float, gqa.y);
-      cd = Best<T>{(T)gqv, gqa.w, true};
+      s = (T)__builtin_bit_cast(float, ax);
+      bt = (T)__builtin_bit_cast(float, ay);
+      cd = Best<T>{(T)gqv, aw, true};
       const int ip = lane > 0 ? (int)(gqp & 255u) : -1;
       const uint64_t fm = __ballot(valid && i != ip) & lowmask(lane + 1);
       sl = (i > cq_i0 || cq_l0 == 0) ? 63 - __builtin_clzll(fm) : -1;
@@ -4252,7 +4264,7 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
         cx.misc[5] = n;
         cx.misc[6] = nl_fast;
       }
-      if (tid >= 64 && pf_t >= 0)   // the helper: the flush the previous commit left pending
+      if (helper_wave() && pf_t >= 0)   // the helper: the flush the previous commit left pending
         ring_flush<(WC > 0 ? WC : 512) / 64, RT, true>(rg, rstream, foff, pf_t, pf_lo, pf_hi, nullptr, 0, pf_fp, nrec);
       pf_t = -1;
       __syncthreads();
@@ -4473,7 +4485,7 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
   // helper, after the flush the last commit may have left pending; its
   // stream cursor is then the item's record count)
   if constexpr (HW) {
-    if (R > 0 && sl > 0 && tid >= 64) {
+    if (R > 0 && sl > 0 && helper_wave()) {
       if (pf_t >= 0) ring_flush<(WC > 0 ? WC : 512) / 64, RT, true>(rg, rstream, foff, pf_t, pf_lo, pf_hi, nullptr, 0, pf_fp, nrec);
       ring_flush<(WC > 0 ? WC : 512) / 64, RT, true>(rg, rstream, foff, sl - 1, flushed, sl - 1, cx.tops, np, nflush, nrec);
       if (tid == 64) misc[13] = nrec;
