@@ -44,8 +44,10 @@ hipError_t ctcx_gstate_launch_decode(const void* p, int is_f64, int scored, hipS
 
 static thread_local std::string g_err;
 
-// the two-wave kernels a call runs by default (ctcx::helper_kind's mode)
-constexpr int kDefaultHelperMode = ctcx::kHelperLegacy;
+// the two-wave kernels a call runs by default (ctcx::helper_kind's mode): the
+// scored gather queue for beams <= 128 (cfg3 decode 144.9 -> 126.8 ms, cfg4
+// 164.9 -> 162.9 ms, same box: profiles/r5j_ab.txt), the gather queue above
+constexpr int kDefaultHelperMode = ctcx::kHelperScored;
 
 static int fail(int code, const std::string& msg) {
   g_err = msg;

@@ -38,6 +38,12 @@ FAMILIES = {
     # full, larger C, ties deciding the bottom)
     "gstate_large_c": (5014, dict(T_max=15, B_max=2, C_min=65, C_max=600, W_min=4, W_max=64, flags="gstate")),
     "gstate_ties": (5015, dict(T_max=20, B_max=2, C_max=40, W_max=48, ties=True, flags="gstate")),
+    # round 5: the scored gather queue (beams <= 128, any C): re-offers,
+    # deactivations and turns closing inside compacted chunks, ties deciding
+    # the bottom the helper gathers against
+    "sq_reoffer": (5016, dict(T_max=60, B_max=3, C_max=6, W_max=12, ties=True)),
+    "sq_cfg3_ties": (5017, dict(T_max=80, B_max=2, C_min=20, C_max=40, W_min=60, W_max=128, ties=True)),
+    "sq_large_c_ties": (5018, dict(T_max=30, B_max=2, C_min=65, C_max=600, W_min=8, W_max=128, ties=True)),
 }
 total = 0
 t0 = time.time()
