@@ -2838,7 +2838,10 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
             // the grow of this frame and of every later one ends, no queue
             // slot is used)
             uint64_t tw = 0;
+            const uint64_t tq0 = pc ? __builtin_amdgcn_s_memtime() : 0;
+            int spins = 0;
             for (int spin = 0;; ++spin) {
+              spins = spin + 1;
               __builtin_amdgcn_s_sleep(CTCX_SLEEP);
               if (ctl_ld(cx.misc, kCtlReady) > gqc) break;
               if (ctl_ld(cx.misc, kCtlDead) != 0 || wait_expired(spin, tw)) {   // never in a correct run
@@ -2849,6 +2852,12 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
             }
             __asm__ volatile("" ::: "memory");
             read_slot();
+            if (pc) {   // diagnostics: the queue wait (its s_sleep rounds); gqc 0: the frame's first chunk
+              (void)uni((int)h0);
+              pc[19] += __builtin_amdgcn_s_memtime() - tq0;
+              pc[20] += spins;
+              if (gqc == 0) pc[14] += __builtin_amdgcn_s_memtime() - tq0;
+            }
           }
         }
         __asm__ volatile("" ::: "memory");

@@ -44,8 +44,9 @@ for b in o[-3:][::-1]:
         b, buf[b, 6] / fr, buf[b, 3] / fr, buf[b, 2] / fr, buf[b, 9] / fr, buf[b, 8] / fr))
 print("  mean heap events/frame %.1f, max %.1f" % (buf[:, 6].mean() / fr, buf[:, 6].max() / fr))
 # two-wave kernels (cfg2/cfg3 class): the score-table wait and where the waves ran
-if len(sys.argv) <= 5 or int(sys.argv[5]) <= 64:
-    print("  HW table wait %.0f cycles/frame, %.2f s_sleep rounds/frame" % (m[19] / fr, m[20] / fr))
+if True:
+    print("  HW table / queue wait %.0f cycles/frame, %.2f s_sleep rounds/frame (first chunk: %.0f cycles)"
+          % (m[19] / fr, m[20] / fr, m[14] / fr))
     w0, w1 = buf[:, 21].astype(np.int64), buf[:, 22].astype(np.int64)
     simd0, simd1 = (w0 >> 4) & 3, (w1 >> 4) & 3
     cu0, cu1 = (w0 >> 8) & 15, (w1 >> 8) & 15
