@@ -2078,7 +2078,7 @@ __device__ __forceinline__ void sq_score(const Ctx<T>& cx, int buf, T norm, bool
 template <typename T>
 __device__ __forceinline__ void gather_small_scored(const Ctx<T>& cx, int buf, int nb, T norm, T bottom, int& i0,
                                                     int& li0, bool& gstop, CTCX_LDS u32x4* qa, CTCX_LDS float* qp,
-                                                    int& cqn) {
+                                                    int& cqn, bool one_step) {
   const int lane = threadIdx.x & 63;
   const int Cm1 = cx.C - 1, blank = cx.blank;
   const float rcp = 1.0f / (float)Cm1;
@@ -2129,12 +2129,23 @@ __device__ __forceinline__ void gather_small_scored(const Ctx<T>& cx, int buf, i
     qa2 += ((qa2 + 1) * Cm1 <= xa) ? 1 : 0;
     i0 += qa2;
     li0 = xa - qa2 * Cm1;
-    if (gstop) break;
+    if (gstop || (one_step && cqn > 0)) break;
   }
 }
 
-// The scored gather queue's helper (SQ kernels): as help_gather_chunks, one
-// chunk ahead of wave 0 (lead 1), each chunk's offers scored (sq_score).
+// The scored gather queue's helper (SQ kernels): as help_gather_chunks, up to
+// kSqLead chunks ahead of wave 0, each chunk's offers scored (sq_score).
+// small C: two ahead (cfg3 decode 124.9 -> 123.4 ms, same box); large C: one
+// (two costs cfg4 +1.6%: chunks gathered against older bottoms carry more
+// offers wave 0 then rejects)
+#ifndef CTCX_SQ_LEAD
+#define CTCX_SQ_LEAD 2
+#endif
+#ifndef CTCX_SQ_FIRST1
+#define CTCX_SQ_FIRST1 1
+#endif
+constexpr int kSqLead = CTCX_SQ_LEAD;   // (small C; large C gathers one ahead)
+constexpr bool kSqFirst1 = CTCX_SQ_FIRST1 != 0;
 template <typename T, bool BIG>
 __device__ __forceinline__ void help_gather_scored(const Ctx<T>& cx, GQ q, int buf, int nb, T norm, T pmax,
                                                    T bottom) {
@@ -2149,14 +2160,14 @@ __device__ __forceinline__ void help_gather_scored(const Ctx<T>& cx, GQ q, int b
   for (int c = 0;; ++c) {
     bool done = false;
     uint64_t tw = 0;
-    for (int spin = 0;; ++spin) {   // the grow still running, and wave 0 at most one chunk behind
+    for (int spin = 0;; ++spin) {   // the grow still running, and wave 0 at most kSqLead chunks behind
       if (ctl_ld(m, kCtlDone) != 0) { done = true; break; }
       if (wait_expired(spin, tw)) {
         __hip_atomic_store(&m[kCtlDead], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         done = true;
         break;
       }
-      if (c <= ctl_ld(m, kCtlCons)) break;
+      if (c < ctl_ld(m, kCtlCons) + (BIG ? 1 : kSqLead)) break;
       __builtin_amdgcn_s_sleep(CTCX_SLEEP);
     }
     if (done) break;
@@ -2198,7 +2209,10 @@ __device__ __forceinline__ void help_gather_scored(const Ctx<T>& cx, GQ q, int b
         qp[lane] = (float)cd.p;
       }
     } else {
-      gather_small_scored<T>(cx, buf, nb, norm, bottom, i0, li0, gstop, qa, qp, cqn);
+      // the frame's first chunk: the first scan step's offers only, so wave 0
+      // starts after one step instead of a full chunk (the helper gathers the
+      // next chunk meanwhile)
+      gather_small_scored<T>(cx, buf, nb, norm, bottom, i0, li0, gstop, qa, qp, cqn, kSqFirst1 && c == 0);
     }
     if (lane == 0) {
       q.h[slot * 4 + 0] = cqn;
