@@ -1757,7 +1757,7 @@ __device__ __forceinline__ void help_score_chunks(const Ctx<T>& cx, Tab tb, int 
 template <typename T>
 __device__ __forceinline__ void gather_chunk(const Ctx<T>& cx, int buf, int nb, T norm, T pmax, T bottom, int tsn,
                                              T txo, int& i0, int& li0, int& cbr, bool& gstop,
-                                             CTCX_LDS uint32_t* cq, int& cqn, uint64_t* pc) {
+                                             CTCX_LDS uint32_t* cq, int& cqn, uint64_t* pc, int cap = 64) {
   const int lane = threadIdx.x & 63;
   const T NI = ninf<T>();
   const int Cm1 = cx.C - 1;
@@ -1776,7 +1776,7 @@ __device__ __forceinline__ void gather_chunk(const Ctx<T>& cx, int buf, int nb, 
     const uint64_t tg0 = pc ? __builtin_amdgcn_s_memtime() : 0;
     const T tsx = lane < tsn ? (T)row_topx(cx)[lane] : NI;                          // S in label-index order:
     const int tsl = lane < tsn ? ((CTCX_LDS int*)(row_topx(cx) + kTopK))[lane] : Cm1;   // lane j its j-th
-    while (cqn < 64) {
+    while (cqn < cap) {
       const uint64_t te0 = pc ? __builtin_amdgcn_s_memtime() : 0;
       if (enter) {
         // the next branch with a turn closed (stop), or with something to
@@ -1846,7 +1846,7 @@ __device__ __forceinline__ void gather_chunk(const Ctx<T>& cx, int buf, int nb, 
             const bool h = lane < tsn && ((sxv + ob) > bottom);
             const uint64_t hM = __ballot(h);
             const int nh = __builtin_popcountll(hM);
-            if (nh > 64 - cqn) break;
+            if (nh > cap - cqn) break;
             if (h) {
               const int r = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(hM >> 32),
                                                            __builtin_amdgcn_mbcnt_lo((unsigned)hM, 0u));
@@ -1883,7 +1883,7 @@ __device__ __forceinline__ void gather_chunk(const Ctx<T>& cx, int buf, int nb, 
                 bits &= bits - 1ull;
                 if (__ballot(hot && tsl == xc)) continue;   // also a hot offer of S
                 const int pos = cqn + __builtin_popcountll(hotM & __ballot(tsl < xc)) + nch;
-                if (lane == 0 && pos < 64) cq[pos] = ((uint32_t)i0 << 16) | (uint32_t)xc;
+                if (lane == 0 && pos < cap) cq[pos] = ((uint32_t)i0 << 16) | (uint32_t)xc;
                 padd += (tsl > xc) ? 1 : 0;
                 ++nch;
               }
@@ -1891,7 +1891,7 @@ __device__ __forceinline__ void gather_chunk(const Ctx<T>& cx, int buf, int nb, 
           }
         }
         if (pc) pc[23] += __builtin_amdgcn_s_memtime() - te0;
-        if (nh + nch <= 64 - cqn) {
+        if (nh + nch <= cap - cqn) {
           if (hot) {
             const int r = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(hotM >> 32),
                                                          __builtin_amdgcn_mbcnt_lo((unsigned)hotM, 0u));
@@ -1959,7 +1959,7 @@ __device__ __forceinline__ void gather_chunk(const Ctx<T>& cx, int buf, int nb, 
         int endw = 0;
 #pragma unroll
         for (int j = 0; j < kGatherWin; ++j) {
-          if (aw[j] >= 0 && nli0 < 0 && cqn < 64) {
+          if (aw[j] >= 0 && nli0 < 0 && cqn < cap) {
             const int wb = aw[j] * 64;
             const int x = wb + lane;
             const bool hot = x >= li0 && x < Cm1 &&
@@ -1967,8 +1967,8 @@ __device__ __forceinline__ void gather_chunk(const Ctx<T>& cx, int buf, int nb, 
             uint64_t hotM = __ballot(hot);
             const int rank =
                 (int)__builtin_amdgcn_mbcnt_hi((unsigned)(hotM >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)hotM, 0u));
-            if (__builtin_popcountll(hotM) > 64 - cqn) {   // the chunk fills here
-              hotM = __ballot(hot && rank < 64 - cqn);
+            if (__builtin_popcountll(hotM) > cap - cqn) {   // the chunk fills here
+              hotM = __ballot(hot && rank < cap - cqn);
               nli0 = wb + 64 - __builtin_clzll(hotM);
             }
             if ((hotM >> lane) & 1ull) cq[cqn + rank] = ((uint32_t)i0 << 16) | (uint32_t)x;
@@ -2146,6 +2146,10 @@ __device__ __forceinline__ void gather_small_scored(const Ctx<T>& cx, int buf, i
 #endif
 constexpr int kSqLead = CTCX_SQ_LEAD;   // (small C; large C gathers one ahead)
 constexpr bool kSqFirst1 = CTCX_SQ_FIRST1 != 0;
+#ifndef CTCX_SQ_CAP0
+#define CTCX_SQ_CAP0 32
+#endif
+constexpr int kSqCap0 = CTCX_SQ_CAP0;   // large C: offers in the frame's first chunk (cfg4: 16, 32, 64 within 0.2%)
 template <typename T, bool BIG>
 __device__ __forceinline__ void help_gather_scored(const Ctx<T>& cx, GQ q, int buf, int nb, T norm, T pmax,
                                                    T bottom) {
@@ -2187,7 +2191,9 @@ __device__ __forceinline__ void help_gather_scored(const Ctx<T>& cx, GQ q, int b
       // array first; each lane then scores its entry and overwrites its own
       // value word
       CTCX_LDS uint32_t* sc = (CTCX_LDS uint32_t*)qp;
-      gather_chunk<T>(cx, buf, nb, norm, pmax, bottom, tsn, txo, i0, li0, cbr, gstop, sc, cqn, nullptr);
+      // (the frame's first chunk capped at kSqCap0 offers, so wave 0 starts sooner)
+      gather_chunk<T>(cx, buf, nb, norm, pmax, bottom, tsn, txo, i0, li0, cbr, gstop, sc, cqn, nullptr,
+                      c == 0 ? kSqCap0 : 64);
       wsync<true>();
       const bool v = lane < cqn;
       const uint32_t e = sc[v ? lane : 0];
