@@ -54,7 +54,10 @@ def main():
     f_rows = known["calib_rows"] / (c_rows * 1024)
     f_s16 = known["calib_stream16"] / (c_s16 * 1024)
     f_rec = known[kname] / (c_rec * 1024)
-    rd = fetch * 1024 * f_rows
+    # the decode kernel's row reads: 4 B/lane (C <= 64, the default) or, for
+    # large C, batches of 16-byte loads (READ_PATTERN=stream16)
+    pattern = os.environ.get("READ_PATTERN", "rows4")
+    rd = fetch * 1024 * (f_s16 if pattern == "stream16" else f_rows)
     wr = write * 1024 * f_rec
     with open(LIB, "rb") as f:
         sha = hashlib.sha256(f.read()).hexdigest()[:16]
@@ -62,7 +65,8 @@ def main():
         "config": cfg, "seq_len": int(seq_len), "kernel": name, "lib_sha16": sha,
         "fetch_size_kb_raw": fetch, "write_size_kb_raw": write, "launches": [nf, nw],
         "calibration": {"fetch_factor_rows_4B_lane": f_rows, "fetch_factor_stream_16B_lane": f_s16,
-                        "write_factor_records": f_rec, "record_bytes": rb, "tool": "tools/fetch_calib.hip"},
+                        "write_factor_records": f_rec, "record_bytes": rb, "read_pattern": pattern,
+                        "tool": "tools/fetch_calib.hip"},
         "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
         "hbm_bytes_per_launch": rd + wr,
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
