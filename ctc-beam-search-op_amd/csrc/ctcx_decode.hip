@@ -2012,25 +2012,35 @@ struct GQ {
   CTCX_LDS int* h;          // [slot][4]: cqn, span start (branch, label index), gstop
   CTCX_LDS u32x4* a;        // [slot][64]: scored offers (SQ)
   CTCX_LDS float* p;        // [slot][64]: their candidate values (SQ)
+  int sm;                   // slots - 1 (a power of two)
 };
-__host__ __device__ inline size_t gq_lds_bytes(bool scored = false) {
-  return (size_t)kQSlots * ((scored ? 64 * 20 : 64 * 4) + 16);
+// Scored slots per kernel: four for beams <= 128; one for beams of 129..256,
+// whose layout must stay under half a CU (cfg5: 80.1 KB of the 80 KB, a
+// scored slot 1.3 KB) -- with one slot the helper gathers chunk c + 1 while
+// wave 0 runs chunk c (wave 0 has read the slot before it publishes kCtlCons)
+__host__ __device__ constexpr int sq_slots(int wcap) { return wcap <= 128 ? kQSlots : 1; }
+__host__ __device__ inline size_t gq_lds_bytes(bool scored, int slots = kQSlots) {
+  return (size_t)slots * ((scored ? 64 * 20 : 64 * 4) + 16);
 }
 template <bool SCORED>
-__device__ __forceinline__ GQ gq_carve(CTCX_LDS char* p) {
+__device__ __forceinline__ GQ gq_carve(CTCX_LDS char* p, int slots) {
   GQ q{};
+  q.sm = slots - 1;
   if constexpr (SCORED) {
     q.a = (CTCX_LDS u32x4*)p;
-    q.p = (CTCX_LDS float*)(p + (size_t)kQSlots * 64 * 16);
-    q.h = (CTCX_LDS int*)(p + (size_t)kQSlots * 64 * 20);
+    q.p = (CTCX_LDS float*)(p + (size_t)slots * 64 * 16);
+    q.h = (CTCX_LDS int*)(p + (size_t)slots * 64 * 20);
   } else {
     q.e = (CTCX_LDS uint32_t*)p;
-    q.h = (CTCX_LDS int*)(p + (size_t)kQSlots * 64 * 4);
+    q.h = (CTCX_LDS int*)(p + (size_t)slots * 64 * 4);
   }
   return q;
 }
+// a scored offer's packed word: branch (bits 0-7), branch child + 1 (8-16),
+// label (17-31; the scored queue runs for C <= kSqMaxClasses)
+constexpr int kSqMaxClasses = 32768;
 __device__ __forceinline__ uint32_t sq_pack(int i, int cw, int l) {
-  return (uint32_t)i | ((uint32_t)(cw + 1) << 8) | ((uint32_t)l << 16);
+  return (uint32_t)i | ((uint32_t)(cw + 1) << 8) | ((uint32_t)l << 17);
 }
 
 // One offer's scored fields, from the frame-start state only (what the
@@ -2181,7 +2191,7 @@ __device__ __forceinline__ void help_gather_scored(const Ctx<T>& cx, GQ q, int b
 #ifdef CTCX_SQ_NOFILTER   // (diagnostics: every offer gathered, no closed turn found here)
     bottom = ninf<T>();
 #endif
-    const int slot = c % kQSlots;
+    const int slot = c & q.sm;
     const int s_i0 = i0, s_l0 = li0;
     int cqn = 0;
     CTCX_LDS u32x4* qa = q.a + slot * 64;
@@ -2259,7 +2269,7 @@ __device__ __forceinline__ void help_gather_chunks(const Ctx<T>& cx, GQ q, int b
     // wave 0's bottom after its last chunk (it only rises)
     const T pb = (T)__builtin_bit_cast(float, (unsigned)ctl_ld(m, kCtlBot));
     bottom = pb > bottom ? pb : bottom;
-    const int slot = c % kQSlots;
+    const int slot = c & q.sm;
     const int s_i0 = i0, s_l0 = li0;
     int cqn = 0;
     gather_chunk<T>(cx, buf, nb, norm, pmax, bottom, tsn, txo, i0, li0, cbr, gstop, q.e + slot * 64, cqn, nullptr);
@@ -2283,7 +2293,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
                           int* n_leaves, uint64_t* pc, Tab tb, GQ gq) {
   // SQ: the scored gather queue (two-wave kernels, beams <= 128, any C): with
   // the beam full, every chunk of the grow comes from the helper scored
-  static_assert(!SQ || (HW && RN == 1), "SQ kernels");
+  static_assert(!SQ || (HW && (RN == 1 || (RN == 2 && BIG))), "SQ kernels");
   uint64_t ts0 = pc ? __builtin_amdgcn_s_memtime() : 0;
   // HW: both waves run up to the recursion, then wave 1 becomes the helper;
   // wave 0 (threadIdx.x == lane) runs the rest
@@ -2830,7 +2840,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       if constexpr (HW) {
         // the next chunk of wave 1's gather queue (the published count is read
         // first, so the reads issued after it see the chunk)
-        const int slot = gqc % kQSlots;
+        const int slot = gqc & gq.sm;
         int h0 = 0, h1 = 0, h2 = 0, h3 = 0;
         auto read_slot = [&]() {
           h0 = gq.h[slot * 4 + 0]; h1 = gq.h[slot * 4 + 1]; h2 = gq.h[slot * 4 + 2]; h3 = gq.h[slot * 4 + 3];
@@ -2924,8 +2934,8 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       const uint32_t ax = gqa.x, ay = gqa.y, az = gqa.z, aw = gqa.w;
       const uint32_t pk = valid ? az : 0u;   // (lanes past cqn: branch 0, no child)
       i = (int)(pk & 255u);
-      c = (int)((pk >> 8) & 255u) - 1;
-      l = (int)(pk >> 16);
+      c = (int)((pk >> 8) & 511u) - 1;
+      l = (int)(pk >> 17);
       s = (T)__builtin_bit_cast(float, ax);
       bt = (T)__builtin_bit_cast(float, ay);
       cd = Best<T>{(T)gqv, aw, true};
@@ -2956,7 +2966,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
               // the branch totals: the slot's (read with the chunk), wave 0's, and the slot's read again now
               g_sq_dbg[3] = (int)__builtin_bit_cast(unsigned, (float)bt);
               g_sq_dbg[4] = (int)__builtin_bit_cast(unsigned, (float)bt2);
-              g_sq_dbg[6] = (int)gq.a[((gqc - 1) % kQSlots) * 64 + lane].y;
+              g_sq_dbg[6] = (int)gq.a[((gqc - 1) & gq.sm) * 64 + lane].y;
               g_sq_dbg[7] = (int)__builtin_bit_cast(unsigned, (float)sel(cx.ot, buf ^ 1)[i]);
               g_sq_dbg[5] = (c & 0xffff) | (c2 << 16);
             }
@@ -4117,7 +4127,7 @@ __device__ void ring_flush(const Ring<RT>& g, RT* out, int32_t* foff, int t_new,
 template <typename T, int RN, int WC, bool BIG, class SC, bool HW, bool SQ = false>
 __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T> prm) {
   static_assert(!HW || (sizeof(T) == 4 && !SC::kStateful && (BIG ? WC > 0 : (RN == 1 && WC == 128))), "HW kernels");
-  static_assert(!SQ || (HW && RN == 1 && WC == 128), "SQ kernels");
+  static_assert(!SQ || (HW && (RN == 1 ? WC == 128 : (RN == 2 && WC == 256 && BIG))), "SQ kernels");
   constexpr int NT = HW ? 128 : 64;
   Ctx<T> cx;
 #ifdef CTCX_GSTATE
@@ -4162,8 +4172,9 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
       off += tab_lds_bytes();
     }
     if constexpr (HW && (BIG || SQ)) {
-      gq = gq_carve<SQ>((CTCX_LDS char*)lds + off);
-      off += gq_lds_bytes(SQ);
+      constexpr int kSlots = SQ ? sq_slots(WC) : kQSlots;
+      gq = gq_carve<SQ>((CTCX_LDS char*)lds + off, kSlots);
+      off += gq_lds_bytes(SQ, kSlots);
     }
     if (R > 0) rg = ring_carve<RT>((CTCX_LDS char*)lds + off, R, W);
   }
@@ -5340,7 +5351,7 @@ hipError_t launch_decode_c(const DecodeParams<T>& p, hipStream_t s) {
   // the decode layout, then (HW) the score table or gather queue, then the
   // record ring (its size by the same functions as the host's checks)
   size_t lds = decode_lds_bytes(WC > 0 ? WC : p.W, p.C, (int)sizeof(T), SC::kStateful);
-  if (HW) lds = ((lds + 15) & ~(size_t)15) + ((BIG || SQ) ? gq_lds_bytes(SQ) : tab_lds_bytes());
+  if (HW) lds = ((lds + 15) & ~(size_t)15) + ((BIG || SQ) ? gq_lds_bytes(SQ, SQ ? sq_slots(WC) : kQSlots) : tab_lds_bytes());
   if (p.ring > 0) lds = ((lds + 15) & ~(size_t)15) + ring_lds_bytes(p.ring, p.W, HW && !BIG ? 4 : 8);
   if (lds > kLdsBytes) return hipErrorInvalidValue;
   if (lds > 64 * 1024) {
@@ -5397,6 +5408,7 @@ hipError_t launch_decode_c(const DecodeParams<T>& p, hipStream_t s) {
 #define CTCX_IF_10(...)
 #define CTCX_IF_11(...)
 #define CTCX_IF_12(...)
+#define CTCX_IF_13(...)
 #if CTCX_PART == 1
 #undef CTCX_IF_1
 #define CTCX_IF_1(...) __VA_ARGS__
@@ -5430,6 +5442,9 @@ hipError_t launch_decode_c(const DecodeParams<T>& p, hipStream_t s) {
 #elif CTCX_PART == 12
 #undef CTCX_IF_12
 #define CTCX_IF_12(...) __VA_ARGS__
+#elif CTCX_PART == 13
+#undef CTCX_IF_13
+#define CTCX_IF_13(...) __VA_ARGS__
 #endif
 #define CTCX_IF_PART(P, ...) CTCX_IF_##P(__VA_ARGS__)
 #if CTCX_PART == 0
@@ -5453,6 +5468,8 @@ extern template hipError_t launch_decode_c<float, 1, 128, false, BaseBeamScorer<
     const DecodeParams<float>&, hipStream_t);
 extern template hipError_t launch_decode_c<float, 1, 128, true, BaseBeamScorer<float>, true, true>(
     const DecodeParams<float>&, hipStream_t);
+extern template hipError_t launch_decode_c<float, 2, 256, true, BaseBeamScorer<float>, true, true>(
+    const DecodeParams<float>&, hipStream_t);
 #else
 CTCX_IF_PART(8, template hipError_t launch_decode_c<float, 1, 128, false, BaseBeamScorer<float>, true>(
                     const DecodeParams<float>&, hipStream_t);)
@@ -5464,6 +5481,9 @@ CTCX_IF_PART(10, template hipError_t launch_decode_c<float, 2, 256, true, BaseBe
 CTCX_IF_PART(11, template hipError_t launch_decode_c<float, 1, 128, false, BaseBeamScorer<float>, true, true>(
                      const DecodeParams<float>&, hipStream_t);)
 CTCX_IF_PART(12, template hipError_t launch_decode_c<float, 1, 128, true, BaseBeamScorer<float>, true, true>(
+                     const DecodeParams<float>&, hipStream_t);)
+// ... and for beams of 129..256 at large C, one slot (part 13)
+CTCX_IF_PART(13, template hipError_t launch_decode_c<float, 2, 256, true, BaseBeamScorer<float>, true, true>(
                      const DecodeParams<float>&, hipStream_t);)
 #endif
 
@@ -5486,7 +5506,7 @@ static hipError_t launch_decode_r(const DecodeParams<T>& p, hipStream_t s) {
 template <typename T>
 int helper_kind(const DecodeParams<T>& p, int mode) {
   if (mode == kHelperNone || sizeof(T) != 4 || p.scorer_tab != nullptr) return 0;
-  if (mode == kHelperScored && p.W <= 128) return 3;
+  if (mode == kHelperScored && p.C <= kSqMaxClasses && (p.W <= 128 || (p.W <= 256 && p.C > 64))) return 3;
   if (p.C <= kRec32MaxClasses) return p.W <= kRec32MaxBeam ? 1 : 0;
   return p.W <= 256 ? 2 : 0;
 }
@@ -5496,7 +5516,7 @@ __host__ inline int helper_wc(int W) { return W <= 128 ? 128 : 256; }
 template <typename T>
 size_t pre_ring_lds_bytes(const DecodeParams<T>& p, int hk, int wc) {
   const size_t b = (decode_lds_bytes(wc, p.C, (int)sizeof(T), p.scorer_tab != nullptr) + 15) & ~(size_t)15;
-  return hk == 1 ? b + tab_lds_bytes() : hk == 2 ? b + gq_lds_bytes(false) : hk == 3 ? b + gq_lds_bytes(true) : b;
+  return hk == 1 ? b + tab_lds_bytes() : hk == 2 ? b + gq_lds_bytes(false) : hk == 3 ? b + gq_lds_bytes(true, sq_slots(wc)) : b;
 }
 // the two-wave kernel this call runs (0: none), given the kind the host chose
 // (hk): its layout and ring must fit
@@ -5534,8 +5554,9 @@ hipError_t launch_decode(const DecodeParams<T>& p, hipStream_t s) {
       return p.W <= 128 ? launch_decode_c<float, 1, 128, true, BaseBeamScorer<float>, true>(p, s)
                         : launch_decode_c<float, 2, 256, true, BaseBeamScorer<float>, true>(p, s);
     if (hk == 3)
-      return p.C > 64 ? launch_decode_c<float, 1, 128, true, BaseBeamScorer<float>, true, true>(p, s)
-                      : launch_decode_c<float, 1, 128, false, BaseBeamScorer<float>, true, true>(p, s);
+      return p.C <= 64   ? launch_decode_c<float, 1, 128, false, BaseBeamScorer<float>, true, true>(p, s)
+             : p.W <= 128 ? launch_decode_c<float, 1, 128, true, BaseBeamScorer<float>, true, true>(p, s)
+                          : launch_decode_c<float, 2, 256, true, BaseBeamScorer<float>, true, true>(p, s);
   }
   if (p.W <= 128) return fits(128) ? launch_decode_r<T, 1, 128>(p, s) : launch_decode_r<T, 1, 0>(p, s);
   if (p.W <= 256) return fits(256) ? launch_decode_r<T, 2, 256>(p, s) : launch_decode_r<T, 2, 0>(p, s);

@@ -1,7 +1,8 @@
 """The two-wave kernels' hand-over forms, each against the oracle on the same
 families (ctcx_decode.hip): CTCEXT_HELPER=1 runs the score table (C <= 64,
 beams <= 128) and the unscored gather queue (C > 64); CTCEXT_HELPER=3 the
-scored gather queue (help_gather_scored: beams <= 128, any C), where the
+scored gather queue (help_gather_scored: beams <= 128 at any C, beams of
+129..256 at C > 64), where the
 helper gathers and scores the offers that can matter against a stale bottom
 and wave 0 pushes them.  Whichever form is the default, the other stays
 covered here; the one-wave kernels are test_gpu_parity.py's CTCEXT_HELPER=0.
@@ -56,7 +57,18 @@ def test_helper_mode_random_large_c(mode):
     _run_random(9316, 4, T_max=16, B_max=2, C_min=2049, C_max=2400, W_min=20, W_max=128, ties=True)
 
 
-@pytest.mark.parametrize("name", sorted(k for k in FULL if FULL[k]["case"][5] <= 128))
+def test_helper_mode_random_large_c_wide(mode):
+    # beams of 129..256 at large C: the scored queue's one-slot form (the RN=2
+    # heap), or the unscored queue four ahead
+    _run_random(9321, 12, T_max=30, B_max=2, C_min=65, C_max=600, W_min=129, W_max=256)
+    assert _stats()["helper"] in mode
+    _run_random(9322, 10, T_max=30, B_max=2, C_min=65, C_max=400, W_min=129, W_max=256, ties=True)
+    _run_random(9323, 8, T_max=30, B_max=2, C_min=66, C_max=200, W_min=129, W_max=256, scale=0.3)
+    _run_random(9324, 6, T_max=40, B_max=2, C_min=300, C_max=1200, W_min=129, W_max=256, scale=2.5)
+    _run_random(9325, 4, T_max=16, B_max=2, C_min=2049, C_max=3000, W_min=129, W_max=256, ties=True)
+
+
+@pytest.mark.parametrize("name", sorted(FULL))
 def test_helper_mode_full_length_golden(name, mode):
     import torch
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
