@@ -692,10 +692,12 @@ extern "C" int ctcext_decode_sharded(ctcext_decoder* d, const ctcext_decode_args
   if (B > 0) {
     // CTCEXT_HELPER (diagnostics, read once per call): 0 the one-wave kernels,
     // 1 the score table / unscored gather queue, 3 the scored gather queue
+    // (beams <= 128; the default), 4 the scored queue for beams <= 256
     const char* hv = getenv("CTCEXT_HELPER");
     const int helper_mode = !hv || !hv[0] ? kDefaultHelperMode
                             : hv[0] == '0' ? ctcx::kHelperNone
-                            : hv[0] == '3' ? ctcx::kHelperScored : ctcx::kHelperLegacy;
+                            : hv[0] == '3' ? ctcx::kHelperScored
+                            : hv[0] == '4' ? ctcx::kHelperScoredWide : ctcx::kHelperLegacy;
     rc = (a->dtype == CTCEXT_F32) ? run_decode<float>(d, a, hsl, s, helper_mode)
                                   : run_decode<double>(d, a, hsl, s, helper_mode);
     if (rc != CTCEXT_OK) return rc;

@@ -5506,7 +5506,9 @@ static hipError_t launch_decode_r(const DecodeParams<T>& p, hipStream_t s) {
 template <typename T>
 int helper_kind(const DecodeParams<T>& p, int mode) {
   if (mode == kHelperNone || sizeof(T) != 4 || p.scorer_tab != nullptr) return 0;
-  if (mode == kHelperScored && p.C <= kSqMaxClasses && (p.W <= 128 || (p.W <= 256 && p.C > 64))) return 3;
+  if ((mode == kHelperScored || mode == kHelperScoredWide) && p.C <= kSqMaxClasses &&
+      (p.W <= 128 || (mode == kHelperScoredWide && p.W <= 256 && p.C > 64)))
+    return 3;
   if (p.C <= kRec32MaxClasses) return p.W <= kRec32MaxBeam ? 1 : 0;
   return p.W <= 256 ? 2 : 0;
 }

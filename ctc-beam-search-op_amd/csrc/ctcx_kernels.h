@@ -154,7 +154,10 @@ struct DecodeParams {
 constexpr int32_t kTestHelperDead = 1;
 // helper_kind's modes and the record size of a two-wave kernel kind (4-byte
 // Rec32 records: the score table, and the scored queue at C <= 64)
-constexpr int kHelperNone = 0, kHelperLegacy = 1, kHelperScored = 3;
+// (kHelperScoredWide: the scored queue for beams of 129..256 too -- measured
+// neutral at cfg5, where the helper's gather alone nearly fills its wave;
+// CTCEXT_HELPER=4, diagnostics)
+constexpr int kHelperNone = 0, kHelperLegacy = 1, kHelperScored = 3, kHelperScoredWide = 4;
 __host__ __device__ inline bool helper_rec32(int hk, int64_t C) { return hk == 1 || (hk == 3 && C <= kRec32MaxClasses); }
 
 struct TraceParams {

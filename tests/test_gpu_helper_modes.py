@@ -21,14 +21,35 @@ from test_gpu_parity import FULL, RMIN, _run_random
 
 pytestmark = pytest.mark.gpu
 
-MODES = {"legacy": ("1", {1, 2}), "scored": ("3", {3})}
+# mode -> CTCEXT_HELPER; the kind a float base-scorer shape then runs
+MODES = {"legacy": "1", "scored": "3", "scored_wide": "4"}
+
+
+def _kind(mode, W, C):
+    if mode != "legacy" and W <= 128:
+        return 3
+    if mode == "scored_wide" and W <= 256 and C > 64:
+        return 3
+    if C <= 64:
+        return 1 if W <= 128 else 0
+    return 2 if W <= 256 else 0
 
 
 @pytest.fixture(params=sorted(MODES))
 def mode(request, monkeypatch):
-    env, kinds = MODES[request.param]
-    monkeypatch.setenv("CTCEXT_HELPER", env)
-    return kinds
+    monkeypatch.setenv("CTCEXT_HELPER", MODES[request.param])
+    return request.param
+
+
+def _check_kind(mode, W, C):
+    assert _stats()["helper"] == _kind(mode, W, C), (mode, W, C, _stats()["helper"])
+
+
+def _probe(mode, W, C):
+    # one decode of a shape the family covers, to check which kernel the mode ran
+    x = np.random.default_rng(W + C).standard_normal((20, 2, C)).astype(np.float32)
+    ctcext_amd.ctc_ext_beam_search_decoder(x, [20, 20], W, 1)
+    _check_kind(mode, W, C)
 
 
 def _stats():
@@ -36,8 +57,8 @@ def _stats():
 
 
 def test_helper_mode_random_small_c(mode):
+    _probe(mode, 100, 29)
     _run_random(9301, 60, W_max=120)
-    assert _stats()["helper"] in mode
     _run_random(9302, 50, ties=True, W_max=120)
     _run_random(9303, 30, neg_inf=True)
     _run_random(9304, 20, flags=RMIN)
@@ -48,8 +69,8 @@ def test_helper_mode_random_small_c(mode):
 
 
 def test_helper_mode_random_large_c(mode):
+    _probe(mode, 100, 300)
     _run_random(9311, 20, T_max=40, B_max=2, C_min=65, C_max=400, W_max=128, scale=4.0)
-    assert _stats()["helper"] in mode
     _run_random(9312, 20, T_max=40, B_max=2, C_min=65, C_max=300, W_max=8, ties=True)
     _run_random(9313, 12, T_max=30, B_max=2, C_min=65, C_max=130, W_min=60, W_max=128, scale=1.5)
     _run_random(9314, 10, T_max=30, B_max=2, C_min=100, C_max=400, W_min=20, W_max=128, ties=True)
@@ -60,8 +81,8 @@ def test_helper_mode_random_large_c(mode):
 def test_helper_mode_random_large_c_wide(mode):
     # beams of 129..256 at large C: the scored queue's one-slot form (the RN=2
     # heap), or the unscored queue four ahead
+    _probe(mode, 200, 300)
     _run_random(9321, 12, T_max=30, B_max=2, C_min=65, C_max=600, W_min=129, W_max=256)
-    assert _stats()["helper"] in mode
     _run_random(9322, 10, T_max=30, B_max=2, C_min=65, C_max=400, W_min=129, W_max=256, ties=True)
     _run_random(9323, 8, T_max=30, B_max=2, C_min=66, C_max=200, W_min=129, W_max=256, scale=0.3)
     _run_random(9324, 6, T_max=40, B_max=2, C_min=300, C_max=1200, W_min=129, W_max=256, scale=2.5)
@@ -81,7 +102,7 @@ def test_helper_mode_full_length_golden(name, mode):
     out = ctcext_amd.ctc_ext_beam_search_decoder(
         torch.as_tensor(x, device="cuda"), torch.as_tensor(sl, device="cuda"),
         W, P, merge_repeated=merge, blank_index=blank, blank_label=blabel)
-    assert _stats()["helper"] in mode
+    _check_kind(mode, W, C)
     di, dv, ds = oracle.pack_sparse(fx["decoded"], B, P)
     ai, av, ash = oracle.pack_sparse(fx["alignment"], B, P)
     lp = np.asarray([[float.fromhex(h) for h in row] for row in fx["log_probability_hex"]], np.float32)
@@ -95,5 +116,5 @@ def test_helper_mode_cfg3_shape(mode):
     x = rng.standard_normal((T, B, C)).astype(np.float32)
     sl = np.array([400, 399, 250, 17], np.int32)
     out = ctcext_amd.ctc_ext_beam_search_decoder(x, sl, W, P, merge_repeated=True)
-    assert _stats()["helper"] in mode
+    _check_kind(mode, W, C)
     compare(out, oracle.decode(x, sl, W, P, True), P)

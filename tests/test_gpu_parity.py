@@ -664,7 +664,7 @@ def test_helper_kernel_selection():
     ctcext_amd.ctc_ext_beam_search_decoder(x2, [20, 20], 100, 1)
     assert _stats()["helper"] == 3 and _stats()["record_bytes"] == 8   # scored queue, large C
     ctcext_amd.ctc_ext_beam_search_decoder(x2, [20, 20], 200, 1)
-    assert _stats()["helper"] == 3 and _stats()["record_bytes"] == 8   # scored queue (one slot), beams > 128
+    assert _stats()["helper"] == 2 and _stats()["record_bytes"] == 8   # gather queue, beams > 128
     ctcext_amd.ctc_ext_beam_search_decoder(x[:, :, :20].copy(), [20, 20], 200, 1)
     assert _stats()["helper"] == 0   # small C, beams > 128: the one-wave kernel
     ctcext_amd.ctc_ext_beam_search_decoder(x.astype(np.float64), [20, 20], 16, 1)
