@@ -622,7 +622,7 @@ def test_record_ring_random_families():
 
 
 def test_record_ring_matches_direct_records():
-    # cfg3's shape at full item length (ragged): the ring (64 frames at W=128:
+    # cfg3's shape at full item length (ragged): the ring (128 frames at W=128:
     # six items, one per CU) and every record written to HBM give the same
     # outputs, and the ring writes fewer records
     rng = np.random.default_rng(77)
@@ -635,11 +635,11 @@ def test_record_ring_matches_direct_records():
     st = dict(_stats())
     b, err = _gpu_or_error(x, sl, W, P, kw, device=True, flags=_lib.CTCEXT_FLAG_NO_RING)
     assert err is None, err
-    assert st["ring_frames"] == 64 and _stats()["ring_frames"] == 0
+    assert st["ring_frames"] == 128 and _stats()["ring_frames"] == 0
     full = _stats()["records_written"]
     # the score-table kernel's default is the ring
     _gpu_or_error(x, sl, W, P, kw, device=True)
-    assert _stats()["ring_frames"] == 64 and _stats()["helper"] == 3
+    assert _stats()["ring_frames"] == 128 and _stats()["helper"] == 3
     assert 0 < st["records_written"] < full, (st["records_written"], full)
     for p in range(P):
         for name in ("decoded_indices", "decoded_values", "decoded_shape",
