@@ -35,6 +35,7 @@
 #include <stdlib.h>
 
 #include <type_traits>
+#include <utility>
 
 #include "ctcx_kernels.h"
 #include "ctcx_topn.h"
@@ -4591,7 +4592,9 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
 // 64-lane loads (the first build read C strided values per thread and
 // reached ~0.2 TB/s).  Two passes over the tiles (max, then sum; for C > 64
 // the max comes from ctcx_row_facts' header); for C <= kNormTile the row
-// stays in LDS between them.
+// stays in LDS between them.  Every float term is exp of x_j - max <= 0 (or
+// NaN): glibc's expf without its range branches (gm::expf_t_nonpos, checked
+// against libm over every such input by tools/check_glibc_math.cpp).
 __host__ __device__ __forceinline__ float norm_exp(float x) { return gm::expf(x); }
 __host__ __device__ __forceinline__ double norm_exp(double x) { return gm::exp(x); }
 __host__ __device__ __forceinline__ float norm_log(float x) { return gm::logf(x); }
@@ -4690,12 +4693,12 @@ __global__ __launch_bounds__(64) void ctcx_row_norm(const T* __restrict__ x, con
             for (int j0 = 0; j0 < kNormTile; j0 += 16) {
               T e[16];
 #pragma unroll
-              for (int j = 0; j < 16; ++j) e[j] = gm::expf_t(tile[lane][j0 + j] - m, etab);
+              for (int j = 0; j < 16; ++j) e[j] = gm::expf_t_nonpos(tile[lane][j0 + j] - m, etab);
 #pragma unroll
               for (int j = 0; j < 16; ++j) s += e[j];
             }
           } else {
-            for (int j = 0; j < nc; ++j) s += gm::expf_t(tile[lane][j] - m, etab);
+            for (int j = 0; j < nc; ++j) s += gm::expf_t_nonpos(tile[lane][j] - m, etab);
           }
         } else {
           for (int j = 0; j < nc; ++j) s += norm_exp(tile[lane][j] - m);
@@ -4704,6 +4707,98 @@ __global__ __launch_bounds__(64) void ctcx_row_norm(const T* __restrict__ x, con
     }
   }
   if (valid) norm[row] = m + norm_log(s);
+}
+
+// ctcx_row_norm for float rows of whole float4s (C % 4 == 0, 16-byte
+// aligned): the same 32-class tiles and class-order sums, moved as 16-byte
+// pieces -- a load instruction covers 8 rows (8 lanes x 16 B each), so 8 loads,
+// 8 LDS writes and 8 LDS reads per lane per tile instead of 32 of each, and
+// each lane's 8 row bases are fetched once, not per tile.
+constexpr int kNormTileW4 = kNormTile + 4;   // 16-byte rows; 36 words apart, b128 row reads conflict-free
+template <int DUMMY = 0>
+__global__ __launch_bounds__(64) void ctcx_row_norm_v4(const float* __restrict__ x, const int32_t* seq_len,
+                                                      float* __restrict__ norm, int64_t Tmax, int64_t B, int64_t C,
+                                                      int64_t xstride, const char* __restrict__ prep) {
+  static_assert(kNormTile == 32, "8 lanes of 16 bytes per tile row");
+  __shared__ __attribute__((aligned(16))) float tile[64][kNormTileW4];
+  __shared__ uint64_t etab[32];
+  const int lane = threadIdx.x;
+  const int64_t rows = Tmax * B;
+  const int64_t row = (int64_t)blockIdx.x * 64 + lane;
+  if (lane < 32) etab[lane] = gm::exp2f_tab(lane);   // read after the first tile's barrier
+  bool valid = false;
+  int64_t off = 0;   // this lane's row, in floats of x (an invalid row: x's first row, never used)
+  if (row < rows) {
+    const int64_t t = row / B, b = row - t * B;
+    valid = t < seq_len[b];
+    if (valid) off = (t * xstride + b) * C;
+  }
+  if (__ballot(valid) == 0ull) return;
+  float m = 0.f, s = 0.f;
+  bool known = false;
+  if (prep != nullptr && valid) {
+    const RowHdr<float> h = *(const RowHdr<float>*)(prep + row * (int64_t)prep_row_bytes(C, 4));
+    if (!h.bad) { m = h.xmax; known = true; }
+  }
+  const bool pass0 = __ballot(valid && !known) != 0ull;
+  // load q covers tile rows 8 q + sub, classes c4 .. c4 + 3 of the tile
+  const int sub = lane >> 3, c4 = (lane & 7) * 4;
+  const float* base[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int src = 8 * q + sub;
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)off, src);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)off >> 32), src);
+    base[q] = x + (int64_t)(((uint64_t)hi << 32) | lo) + c4;
+  }
+  auto load = [&](float4 (&v)[8], int64_t c0) {
+    const bool in = c4 < C - c0;   // (C - c0 is a multiple of 4)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = in ? *(const float4*)(base[q] + c0) : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  float4 v[8];
+  for (int pass = pass0 ? 0 : 1; pass < 2; ++pass) {
+    const bool reload = pass == 0 || C > kNormTile || !pass0;
+    if (reload) load(v, 0);
+    for (int64_t c0 = 0; c0 < C; c0 += kNormTile) {
+      const int nc = (int)(C - c0 < kNormTile ? C - c0 : kNormTile);
+      if (reload) {
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 8; ++q) *(float4*)&tile[8 * q + sub][c4] = v[q];
+        __syncthreads();
+        if (c0 + kNormTile < C) load(v, c0 + kNormTile);
+      }
+      if (valid) {
+        if (pass == 0) {
+          if (!known) {
+            int j = 0;
+            if (c0 == 0) { m = tile[lane][0]; j = 1; }
+            for (; j < nc; ++j) { const float e = tile[lane][j]; m = (e > m) ? e : m; }
+          }
+        } else if (nc == kNormTile) {
+          // a whole tile: 16 exp terms in flight at a time, the sum in class order
+#pragma unroll
+          for (int j0 = 0; j0 < kNormTile; j0 += 16) {
+            float e[16];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float4 w = *(const float4*)&tile[lane][j0 + 4 * i];
+              e[4 * i + 0] = gm::expf_t_nonpos(w.x - m, etab);
+              e[4 * i + 1] = gm::expf_t_nonpos(w.y - m, etab);
+              e[4 * i + 2] = gm::expf_t_nonpos(w.z - m, etab);
+              e[4 * i + 3] = gm::expf_t_nonpos(w.w - m, etab);
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) s += e[j];
+          }
+        } else {
+          for (int j = 0; j < nc; ++j) s += gm::expf_t_nonpos(tile[lane][j] - m, etab);
+        }
+      }
+    }
+  }
+  if (valid) norm[row] = m + gm::logf(s);
 }
 
 #if CTCX_PART == 0
@@ -4917,7 +5012,7 @@ __global__ __launch_bounds__(64) void ctcx_row_prep(const T* __restrict__ x, con
   if (inlds) {
     __syncthreads();
     for (int j = lane; j < Ci; j += 64) {
-      if constexpr (sizeof(T) == 4) xs[j] = gm::expf_t(xs[j] - m, etab);   // glibc expf, its table in LDS
+      if constexpr (sizeof(T) == 4) xs[j] = gm::expf_t_nonpos(xs[j] - m, etab);   // glibc expf, its table in LDS
       else xs[j] = norm_exp(xs[j] - m);
     }
     __syncthreads();
@@ -5015,199 +5110,349 @@ __device__ __forceinline__ unsigned radix_select_desc(const unsigned* cks, int n
   return pfx;
 }
 
+// FUSE: the softmax normaliser too (decoder.h:72-80), from the rows the waves
+// already hold, so the logits are read from HBM once (ctcx_row_norm's second
+// read goes).  The sum stays in class order, one lane per row: after the
+// facts, the block's rows (two per wave) pass through LDS 256 classes at a
+// time as exp terms (two tile buffers over the compact lists, which are done
+// by then), lane q of wave 0 adding row q's tile in class order while the
+// waves write the next one.  A row holding a NaN or +inf (max then in class
+// order) is summed from global memory by its wave's lane 0.  That chain, C
+// dependent adds per block, is the fused kernel's cost: the launcher fuses
+// rows of up to 1024 classes (kFuseNorm; cfg4 0.90 -> 0.75 ms), and past them
+// the second read is cheaper (cfg5 19.4 ms fused against 8.5 + 8.7 split).
+constexpr int kNormTileW = 260;   // floats per tile row: 256 classes + 4 (rows 4 banks apart)
+// f(integral_constant<int, U>) for U in the sequence, in order
+template <typename F, int... U>
+__device__ __forceinline__ void unroll_seq(F& f, std::integer_sequence<int, U...>) {
+  (f(std::integral_constant<int, U>{}), ...);
+}
+// rows per wave: two for the fused kernel's small rows (NV <= 4), whose
+// loads are then in flight together (twice the bytes per wave), and whose
+// normaliser chains are then eight per block
+template <int NV, bool FUSE>
+constexpr int facts_rows_per_wave() { return (FUSE && NV <= 4) ? 2 : 1; }
+// the row widths the launcher fuses the normaliser for (C <= 1024)
 template <int NV>
+constexpr bool kFuseNorm = NV <= 4;
+
+template <int NV, bool FUSE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_WPE, 8))) void ctcx_row_facts(
     const float* __restrict__ x, const int32_t* __restrict__ seq_len, char* __restrict__ prep, int64_t rows,
-    int64_t B, int C, int64_t xstride, int blank) {
+    int64_t B, int C, int64_t xstride, int blank, float* __restrict__ norm) {
   // per wave: the compact list of (key, label index) in label order, with one
   // dummy slot per lane (its stores are unconditional), and the radix histogram
   // (NV <= 4, C <= 1024: 16 keys per lane, bisected in registers as cheaply
   // as a radix select's fixed passes, and no LDS: more waves per SIMD)
   constexpr bool kRadix = NV > 4;
-  __shared__ unsigned cks_all[4][kRadix ? kFactsCompact + 64 : 1];
+  constexpr int R = facts_rows_per_wave<NV, FUSE>();
+  constexpr int NR = 4 * R;   // rows per block: row r * 4 + wave of the block's
+  constexpr int kCks = kRadix ? kFactsCompact + 64 : (FUSE ? 2 * R * kNormTileW : 1);
+  static_assert(!FUSE || 4 * kCks >= 2 * NR * kNormTileW, "the tile buffers fit over the compact lists");
+  __shared__ __attribute__((aligned(16))) unsigned cks_all[4][kCks];
   __shared__ unsigned cls_all[4][kRadix ? kFactsCompact + 64 : 1];
   __shared__ unsigned hist_all[4][kRadix ? 256 : 1];
+  __shared__ uint64_t etab[FUSE ? 32 : 1];   // expf's table (read after the first tile barrier)
+  __shared__ float rmax[FUSE ? NR : 1];   // the rows' maxima, for the summing lanes
+  __shared__ int rsum[FUSE ? NR : 1];     // the rows they sum (live, no NaN / +inf)
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t row = (int64_t)blockIdx.x * 4 + wv;
-  if (row >= rows) return;   // wave-uniform, and no block barrier below
-  const int64_t t = row / B, b = row - t * B;
-  if (t >= seq_len[b]) return;
   const float NI = -__builtin_inff(), PI = __builtin_inff();
   const int C4 = C >> 2;
-  const float4* xr = (const float4*)(x + (t * xstride + b) * (int64_t)C);
-  char* pr = prep + row * (int64_t)prep_row_bytes(C, 4);
-  float* bm = (float*)(pr + prep_bmax_offset(4));
-  uint2* top = (uint2*)(pr + prep_top_offset(C, 4));
-  const int nblk = (C + 63) / 64;
-  // the row, then its keys: fkey of each non-blank class, 0 for the blank and
-  // the padding (fkey is order-preserving; 0 is the key of one NaN pattern
+  if constexpr (FUSE) {
+    if (threadIdx.x < 32) etab[threadIdx.x] = gm::exp2f_tab(threadIdx.x);
+  }
+  // the rows, then their keys: fkey of each non-blank class, 0 for the blank
+  // and the padding (fkey is order-preserving; 0 is the key of one NaN pattern
   // only, and a row holding a NaN is decoded literally, without S)
-  unsigned k[NV][4];
-  // buffer loads: one lane offset and a constant row offset per load, no
-  // 64-bit address per load in flight (those took 40 VGPRs at NV = 20); past
-  // the row they return 0, replaced by -inf below
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)xr, (short)0, C * 4, 0x00020000);
+  unsigned kr[R][NV][4];
+  int64_t rrow[R];
+  bool live[R], rbad[R];
+  float rxmax[R], xbv[R];   // FUSE: the blank's value, whose key is 0, for its exp term
 #pragma unroll
-  for (int u = 0; u < NV; ++u) {
-    const auto f = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, u * 1024, 0);
-    k[u][0] = f[0]; k[u][1] = f[1]; k[u][2] = f[2]; k[u][3] = f[3];
-  }
-  // maximum, NaN / +inf, the block maxima (block 4 u + (lane >> 4) is the
-  // 16-lane DPP row of one u: its maximum lands on the row's lane 15), and
-  // the lane's largest key
-  float xmax = NI;
-  bool bad = false;
-  unsigned lk = 0u;
-  const int bl4 = blank - 4 * lane;
-#pragma unroll
-  for (int u = 0; u < NV; ++u) {
-    float lm = NI;
-    const bool inrow = 64 * u + lane < C4;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const float v = inrow ? __uint_as_float(k[u][c]) : NI;
-      bad |= (v != v) || (v == PI);
-      lm = v > lm ? v : lm;
-      // class 4 lane + 256 u + c is the blank iff 256 u + c == bl4 (no class
-      // index per element: kept for the compaction, 80 of them took 80 VGPRs);
-      // bitwise &: no short-circuit branch, so the key takes the value's register
-      const unsigned kv = fkey(v);
-      k[u][c] = (inrow & (256 * u + c != bl4)) ? kv : 0u;
-      lk = k[u][c] > lk ? k[u][c] : lk;
+  for (int r = 0; r < R; ++r) {
+    const int64_t row = (int64_t)blockIdx.x * NR + r * 4 + wv;
+    const int64_t t = row / B, b = row - t * B;
+    rrow[r] = row;
+    if constexpr (FUSE) {
+      live[r] = row < rows && t < seq_len[b];   // wave-uniform; every wave reaches the tile barriers below
+    } else {
+      if (row >= rows) return;   // wave-uniform, and no block barrier below
+      if (t >= seq_len[b]) return;
+      live[r] = true;
     }
-    xmax = lm > xmax ? lm : xmax;
-    float w;
-    w = dpp_f<0x111>(lm, NI); lm = w > lm ? w : lm;
-    w = dpp_f<0x112>(lm, NI); lm = w > lm ? w : lm;
-    w = dpp_f<0x114>(lm, NI); lm = w > lm ? w : lm;
-    w = dpp_f<0x118>(lm, NI); lm = w > lm ? w : lm;
-    const int kb = 4 * u + (lane >> 4);
-    if ((lane & 15) == 15 && 64 * u < C4 && kb < nblk) bm[kb] = lm;
-  }
-  RowHdr<float> h;
-  h.xmax = wave_max_dpp(xmax);
-  h.bad = __ballot(bad) != 0ull;
-  const int K = kTopK;
-  auto unkey = [](unsigned kv) { return kv ^ ((kv >> 31) ? 0x80000000u : 0xFFFFFFFFu); };   // fkey's inverse
-  const uint64_t ltm = (1ull << lane) - 1ull;
-  // S = the keys >= tau, tau the smallest threshold with |S| <= K: one past
-  // the (K+1)-th largest key v, and the largest key outside S is then v
-  // itself (C - 1 <= K: every label, nothing outside).  The smallest lane
-  // maximum km bounds v from below: one key per lane at or above it (when
-  // every lane holds a label, C >= 256; else km = 0 and the bound is 1).
-  const unsigned km = (unsigned)uni((int)wave_min_dpp(lk));
-  const unsigned kmx = (unsigned)uni((int)~wave_min_dpp(~lk));   // the largest key
-  const unsigned kt = km > 1u ? km : 1u;
-  // every key >= kt into the compact list, in label order (within a u, label
-  // order is (lane, c) order): a label's slot is the count before it
-  unsigned* cks = cks_all[wv];
-  unsigned* cls = cls_all[wv];
-  int n = 0;   // keys >= kt
-  int lb4;   // 4 lane, opaque: recomputed here, not kept from the first pass
-  __asm__ volatile("v_lshlrev_b32 %0, 2, %1" : "=v"(lb4) : "v"(lane));
+    rbad[r] = false;
+    rxmax[r] = NI;
+    xbv[r] = 0.f;
+    if (live[r]) {
+      const float4* xr = (const float4*)(x + (t * xstride + b) * (int64_t)C);
+      if constexpr (FUSE) xbv[r] = ((const float*)xr)[blank];
+      // buffer loads: one lane offset and a constant row offset per load, no
+      // 64-bit address per load in flight (those took 40 VGPRs at NV = 20); past
+      // the row they return 0, replaced by -inf below
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)xr, (short)0, C * 4, 0x00020000);
 #pragma unroll
-  for (int u = 0; u < NV; ++u) {
-    if (kRadix && 64 * u < C4) {   // uniform
-      bool in[4];
-      int before = 0;
-      uint64_t mm[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        in[c] = k[u][c] >= kt;
-        mm[c] = __ballot(in[c]);
-        before += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mm[c] >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mm[c], 0u));
+      for (int u = 0; u < NV; ++u) {
+        const auto f = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, u * 1024, 0);
+        kr[r][u][0] = f[0]; kr[r][u][1] = f[1]; kr[r][u][2] = f[2]; kr[r][u][3] = f[3];
       }
-      int at = n + before;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        // label index: class 4 lane + 256 u + c, less one past the blank
-        const int j = (in[c] && at < kFactsCompact) ? at : kFactsCompact + lane;
-        cks[j] = k[u][c];
-        cls[j] = (unsigned)(lb4 + (256 * u + c) - (256 * u + c > bl4 ? 1 : 0));
-        at += in[c] ? 1 : 0;
-      }
-#pragma unroll
-      for (int c = 0; c < 4; ++c) n += __builtin_popcountll(mm[c]);
     }
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (kRadix && n <= kFactsCompact && (n > K || C - 1 <= K)) {
-    // S from the list: all of it (C - 1 <= K), or the keys above the
-    // (K+1)-th largest, found by a radix select over the list
-    unsigned v = 0u;
-    if (C - 1 > K) v = radix_select_desc(cks, n, K + 1, kt, kmx, hist_all[wv]);
-    int ns = 0;
-    for (int j0 = 0; j0 < n; j0 += 64) {
-      const int j = j0 + lane;
-      const unsigned kv = j < n ? cks[j] : 0u;
-      const bool in = j < n && kv > v;
-      const uint64_t mm = __ballot(in);
-      if (in) {
-        const int r = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mm, 0u));
-        top[ns + r] = make_uint2(unkey(kv), cls[j]);
-      }
-      ns += __builtin_popcountll(mm);
-    }
-    h.ns = ns;
-    h.xout = v == 0u ? NI : __uint_as_float(unkey(v));
-  } else {
-    // NV <= 4, and the rare shapes: exactly K keys at or above km (S is the
-    // list, its outside maximum taken from the registers), or a list past its
-    // capacity (tau bisected over the row's keys, S from the registers)
-    auto cnt_ge = [&](unsigned tau) __attribute__((always_inline)) {
-      int c2 = 0;
+  // the facts of each row, k its values (keys after)
 #pragma unroll
-      for (int u = 0; u < NV; ++u)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) c2 += k[u][c] >= tau ? 1 : 0;
-      return uni(wave_sum_dpp(c2));
-    };
-    if constexpr (!kRadix) n = cnt_ge(kt);
-    unsigned tau = kt;
-    if (n > K) {
-      uint64_t lo = kt - 1u, hi = (uint64_t)kmx + 1ull;   // cnt(lo) >= cnt(kt) > K >= cnt(hi) = 0
-      while (hi - lo > 1) {
-        const uint64_t mid = (lo + hi) >> 1;
-        const int c2 = cnt_ge((unsigned)mid);
-        if (c2 <= K) hi = mid;
-        else lo = mid;
-        if (c2 == K) break;
-      }
-      tau = (unsigned)hi;
-    }
-    unsigned ko = 0u;
-    int ns = 0;
+  for (int r = 0; r < R; ++r) {
+    if (!live[r]) continue;   // wave-uniform
+    const int64_t row = rrow[r];
+    unsigned (&k)[NV][4] = kr[r];
+    char* pr = prep + row * (int64_t)prep_row_bytes(C, 4);
+    float* bm = (float*)(pr + prep_bmax_offset(4));
+    uint2* top = (uint2*)(pr + prep_top_offset(C, 4));
+    const int nblk = (C + 63) / 64;
+    // maximum, NaN / +inf, the block maxima (block 4 u + (lane >> 4) is the
+    // 16-lane DPP row of one u: its maximum lands on the row's lane 15), and
+    // the lane's largest key
+    float xmax = NI;
+    bool bad = false;
+    unsigned lk = 0u;
+    const int bl4 = blank - 4 * lane;
 #pragma unroll
     for (int u = 0; u < NV; ++u) {
-      if (64 * u < C4) {   // uniform
+      float lm = NI;
+      const bool inrow = 64 * u + lane < C4;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float v = inrow ? __uint_as_float(k[u][c]) : NI;
+        bad |= (v != v) || (v == PI);
+        lm = v > lm ? v : lm;
+        // class 4 lane + 256 u + c is the blank iff 256 u + c == bl4 (no class
+        // index per element: kept for the compaction, 80 of them took 80 VGPRs);
+        // bitwise &: no short-circuit branch, so the key takes the value's register
+        const unsigned kv = fkey(v);
+        k[u][c] = (inrow & (256 * u + c != bl4)) ? kv : 0u;
+        lk = k[u][c] > lk ? k[u][c] : lk;
+      }
+      xmax = lm > xmax ? lm : xmax;
+      float w;
+      w = dpp_f<0x111>(lm, NI); lm = w > lm ? w : lm;
+      w = dpp_f<0x112>(lm, NI); lm = w > lm ? w : lm;
+      w = dpp_f<0x114>(lm, NI); lm = w > lm ? w : lm;
+      w = dpp_f<0x118>(lm, NI); lm = w > lm ? w : lm;
+      const int kb = 4 * u + (lane >> 4);
+      if ((lane & 15) == 15 && 64 * u < C4 && kb < nblk) bm[kb] = lm;
+    }
+    RowHdr<float> h;
+    h.xmax = wave_max_dpp(xmax);
+    h.bad = __ballot(bad) != 0ull;
+    const int K = kTopK;
+    auto unkey = [](unsigned kv) { return kv ^ ((kv >> 31) ? 0x80000000u : 0xFFFFFFFFu); };   // fkey's inverse
+    const uint64_t ltm = (1ull << lane) - 1ull;
+    // S = the keys >= tau, tau the smallest threshold with |S| <= K: one past
+    // the (K+1)-th largest key v, and the largest key outside S is then v
+    // itself (C - 1 <= K: every label, nothing outside).  The smallest lane
+    // maximum km bounds v from below: one key per lane at or above it (when
+    // every lane holds a label, C >= 256; else km = 0 and the bound is 1).
+    const unsigned km = (unsigned)uni((int)wave_min_dpp(lk));
+    const unsigned kmx = (unsigned)uni((int)~wave_min_dpp(~lk));   // the largest key
+    const unsigned kt = km > 1u ? km : 1u;
+    // every key >= kt into the compact list, in label order (within a u, label
+    // order is (lane, c) order): a label's slot is the count before it
+    unsigned* cks = cks_all[wv];
+    unsigned* cls = cls_all[wv];
+    int n = 0;   // keys >= kt
+    int lb4;   // 4 lane, opaque: recomputed here, not kept from the first pass
+    __asm__ volatile("v_lshlrev_b32 %0, 2, %1" : "=v"(lb4) : "v"(lane));
+#pragma unroll
+    for (int u = 0; u < NV; ++u) {
+      if (kRadix && 64 * u < C4) {   // uniform
         bool in[4];
-        uint64_t mm[4];
         int before = 0;
+        uint64_t mm[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          in[c] = k[u][c] >= tau;
-          if (!in[c]) ko = k[u][c] > ko ? k[u][c] : ko;
+          in[c] = k[u][c] >= kt;
           mm[c] = __ballot(in[c]);
-          before += __builtin_popcountll(mm[c] & ltm);
+          before += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mm[c] >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mm[c], 0u));
         }
+        int at = n + before;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          if (in[c]) {
-            top[ns + before] = make_uint2(unkey(k[u][c]), (unsigned)(lb4 + (256 * u + c) - (256 * u + c > bl4 ? 1 : 0)));
-            ++before;
-          }
+          // label index: class 4 lane + 256 u + c, less one past the blank
+          const int j = (in[c] && at < kFactsCompact) ? at : kFactsCompact + lane;
+          cks[j] = k[u][c];
+          cls[j] = (unsigned)(lb4 + (256 * u + c) - (256 * u + c > bl4 ? 1 : 0));
+          at += in[c] ? 1 : 0;
         }
 #pragma unroll
-        for (int c = 0; c < 4; ++c) ns += __builtin_popcountll(mm[c]);
+        for (int c = 0; c < 4; ++c) n += __builtin_popcountll(mm[c]);
       }
     }
-    h.ns = ns;
-    ko = (unsigned)uni((int)~wave_min_dpp(~ko));   // the wave's largest
-    h.xout = ko == 0u ? NI : __uint_as_float(unkey(ko));
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (kRadix && n <= kFactsCompact && (n > K || C - 1 <= K)) {
+      // S from the list: all of it (C - 1 <= K), or the keys above the
+      // (K+1)-th largest, found by a radix select over the list
+      unsigned v = 0u;
+      if (C - 1 > K) v = radix_select_desc(cks, n, K + 1, kt, kmx, hist_all[wv]);
+      int ns = 0;
+      for (int j0 = 0; j0 < n; j0 += 64) {
+        const int j = j0 + lane;
+        const unsigned kv = j < n ? cks[j] : 0u;
+        const bool in = j < n && kv > v;
+        const uint64_t mm = __ballot(in);
+        if (in) {
+          const int r = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mm, 0u));
+          top[ns + r] = make_uint2(unkey(kv), cls[j]);
+        }
+        ns += __builtin_popcountll(mm);
+      }
+      h.ns = ns;
+      h.xout = v == 0u ? NI : __uint_as_float(unkey(v));
+    } else {
+      // NV <= 4, and the rare shapes: exactly K keys at or above km (S is the
+      // list, its outside maximum taken from the registers), or a list past its
+      // capacity (tau bisected over the row's keys, S from the registers)
+      auto cnt_ge = [&](unsigned tau) __attribute__((always_inline)) {
+        int c2 = 0;
+#pragma unroll
+        for (int u = 0; u < NV; ++u)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) c2 += k[u][c] >= tau ? 1 : 0;
+        return uni(wave_sum_dpp(c2));
+      };
+      if constexpr (!kRadix) n = cnt_ge(kt);
+      unsigned tau = kt;
+      if (n > K) {
+        uint64_t lo = kt - 1u, hi = (uint64_t)kmx + 1ull;   // cnt(lo) >= cnt(kt) > K >= cnt(hi) = 0
+        while (hi - lo > 1) {
+          const uint64_t mid = (lo + hi) >> 1;
+          const int c2 = cnt_ge((unsigned)mid);
+          if (c2 <= K) hi = mid;
+          else lo = mid;
+          if (c2 == K) break;
+        }
+        tau = (unsigned)hi;
+      }
+      unsigned ko = 0u;
+      int ns = 0;
+#pragma unroll
+      for (int u = 0; u < NV; ++u) {
+        if (64 * u < C4) {   // uniform
+          bool in[4];
+          uint64_t mm[4];
+          int before = 0;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            in[c] = k[u][c] >= tau;
+            if (!in[c]) ko = k[u][c] > ko ? k[u][c] : ko;
+            mm[c] = __ballot(in[c]);
+            before += __builtin_popcountll(mm[c] & ltm);
+          }
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            if (in[c]) {
+              top[ns + before] = make_uint2(unkey(k[u][c]), (unsigned)(lb4 + (256 * u + c) - (256 * u + c > bl4 ? 1 : 0)));
+              ++before;
+            }
+          }
+#pragma unroll
+          for (int c = 0; c < 4; ++c) ns += __builtin_popcountll(mm[c]);
+        }
+      }
+      h.ns = ns;
+      ko = (unsigned)uni((int)~wave_min_dpp(~ko));   // the wave's largest
+      h.xout = ko == 0u ? NI : __uint_as_float(unkey(ko));
+    }
+    if (lane == 0) *(RowHdr<float>*)pr = h;
+    rbad[r] = h.bad;
+    rxmax[r] = h.xmax;
   }
-  if (lane == 0) *(RowHdr<float>*)pr = h;
+  if constexpr (FUSE) {
+    // the exp terms in place of the keys: for a row without NaN / +inf the
+    // maximum is order-free, a key is 0 for the blank and the padding only
+    // (the blank's value is xbv), and -inf gives exp 0
+    auto unkey = [](unsigned kv) { return kv ^ ((kv >> 31) ? 0x80000000u : 0xFFFFFFFFu); };
+    bool sum_row[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      sum_row[r] = live[r] && !rbad[r];   // wave-uniform
+      if (lane == 0) {
+        rmax[r * 4 + wv] = rxmax[r];
+        rsum[r * 4 + wv] = sum_row[r] ? 1 : 0;
+      }
+    }
+    float* const tiles = (float*)&cks_all[0][0];   // [2][NR][kNormTileW]
+    const int bl4 = blank - 4 * lane;
+    __syncthreads();   // the compact lists are done; etab, rmax and rsum are visible
+    float s = 0.f;
+    // the terms of tile u of row r, in place of its keys
+    auto terms = [&](const int r, const int u) __attribute__((always_inline)) {
+      const bool inrow = 64 * u + lane < C4;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float v = (256 * u + c == bl4) ? xbv[r] : __uint_as_float(unkey(kr[r][u][c]));
+        kr[r][u][c] = __float_as_uint(inrow ? gm::expf_t_nonpos(v - rxmax[r], etab) : 0.f);
+      }
+    };
+    // row lane's 256 terms of one tile in class order (zeros past the row add
+    // nothing), the reads one batch ahead of the adds
+    auto chain = [&](const float* tr0) __attribute__((always_inline)) {
+      const float4* tr = (const float4*)tr0;
+      float4 a[2][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[0][i] = tr[i];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        if (q + 1 < 16) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) a[(q + 1) & 1][i] = tr[4 * (q + 1) + i];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          s += a[q & 1][i].x;
+          s += a[q & 1][i].y;
+          s += a[q & 1][i].z;
+          s += a[q & 1][i].w;
+        }
+      }
+    };
+    // one step per tile (u a compile-time index: the rows stay in registers; a
+    // plain loop is not fully unrolled at NV >= 24 and put kr on the stack)
+    auto step = [&](auto uc) __attribute__((always_inline)) {
+      constexpr int u = decltype(uc)::value;
+      if (64 * u >= C4) return;   // block-uniform
+      float* const tb = tiles + (u & 1) * NR * kNormTileW;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (sum_row[r]) {
+          terms(r, u);
+          *(float4*)(tb + (r * 4 + wv) * kNormTileW + 4 * lane) =
+              make_float4(__uint_as_float(kr[r][u][0]), __uint_as_float(kr[r][u][1]), __uint_as_float(kr[r][u][2]),
+                          __uint_as_float(kr[r][u][3]));
+        }
+      }
+      __syncthreads();   // tile u written; tile u - 1's buffer free again
+      if (wv == 0 && lane < NR) chain(tb + lane * kNormTileW);
+    };
+    unroll_seq(step, std::make_integer_sequence<int, NV>{});
+    // (rows with NaN / +inf leave theirs to their own wave, below)
+    if (wv == 0 && lane < NR && rsum[lane]) norm[(int64_t)blockIdx.x * NR + lane] = rmax[lane] + gm::logf(s);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (live[r] && rbad[r] && lane == 0) {
+        // the reference's order for both: maxCoeff's loop, then the sum
+        const int64_t row = rrow[r], t = row / B, b = row - t * B;
+        const float* xr1 = x + (t * xstride + b) * (int64_t)C;
+        float m = xr1[0];
+        for (int j = 1; j < C; ++j) {
+          const float v = xr1[j];
+          m = (v > m) ? v : m;
+        }
+        float s1 = 0.f;
+        for (int j = 0; j < C; ++j) s1 += gm::expf_t(xr1[j] - m, etab);
+        norm[row] = m + gm::logf(s1);
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -5602,11 +5847,43 @@ template int ring_frames<float>(const DecodeParams<float>&, int, int, int);
 template int ring_frames<double>(const DecodeParams<double>&, int, int, int);
 
 template <int NV>
-static hipError_t launch_row_facts(const float* x, const int32_t* sl, char* prep, int64_t rows, int64_t B, int C,
-                                   int64_t xstride, int blank, hipStream_t s) {
-  hipLaunchKernelGGL((ctcx_row_facts<NV>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, x, sl, prep, rows, B,
-                     C, xstride, blank);
+static hipError_t launch_row_facts(const float* x, const int32_t* sl, char* prep, float* norm, int64_t rows,
+                                   int64_t B, int C, int64_t xstride, int blank, bool& fuse, hipStream_t s) {
+  // the normaliser fused for rows of up to 1024 classes only: past them the
+  // block's class-order chain (C dependent adds per four rows) costs more than
+  // the second read it saves (cfg5: 19.4 ms fused, 8.5 + 8.7 split)
+  if constexpr (kFuseNorm<NV>) {
+    if (fuse) {
+      constexpr int nr = 4 * facts_rows_per_wave<NV, true>();
+      hipLaunchKernelGGL((ctcx_row_facts<NV, true>), dim3((unsigned)((rows + nr - 1) / nr)), dim3(256), 0, s, x, sl,
+                         prep, rows, B, C, xstride, blank, norm);
+      return hipGetLastError();
+    }
+  }
+  fuse = false;
+  constexpr int nr = 4 * facts_rows_per_wave<NV, false>();
+  hipLaunchKernelGGL((ctcx_row_facts<NV, false>), dim3((unsigned)((rows + nr - 1) / nr)), dim3(256), 0, s, x, sl,
+                     prep, rows, B, C, xstride, blank, (float*)nullptr);
   return hipGetLastError();
+}
+
+// CTCEXT_NORM_V4=0: ctcx_row_norm instead of ctcx_row_norm_v4 (A/B runs)
+static bool norm_v4() {
+  static const bool v = [] {
+    const char* e = getenv("CTCEXT_NORM_V4");
+    return !(e != nullptr && e[0] == '0');
+  }();
+  return v;
+}
+
+// CTCEXT_PREP_SPLIT=1: the facts and ctcx_row_norm as two kernels (two reads
+// of the logits), the round-4 form, for A/B runs
+static bool prep_split() {
+  static const bool v = [] {
+    const char* e = getenv("CTCEXT_PREP_SPLIT");
+    return e != nullptr && e[0] == '1';
+  }();
+  return v;
 }
 
 template <typename T>
@@ -5616,22 +5893,31 @@ hipError_t launch_row_prep(const T* x, const int32_t* sl, char* prep, T* norm, i
   if (rows == 0 || C <= 64) return hipSuccess;
   if constexpr (sizeof(T) == 4) {
     // float rows of whole float4s (16-byte aligned): the register-resident
-    // row facts, then the rows-per-lane normaliser reading their maxima
+    // row facts, with the normaliser from the same registers (one read) where
+    // that pays, else followed by ctcx_row_norm
     if (C % 4 == 0 && ((uintptr_t)x & 15) == 0 && C <= 256 * 32) {   // NV <= 32 float4 per lane
       const int c4 = (int)(C / 4);
+      bool fuse = !prep_split();   // (cleared by the launcher where it does not fuse)
+      float* nf = (float*)norm;
       hipError_t e;
-      if (c4 <= 64) e = launch_row_facts<1>(x, sl, prep, rows, B, (int)C, xstride, blank, s);
-      else if (c4 <= 128) e = launch_row_facts<2>(x, sl, prep, rows, B, (int)C, xstride, blank, s);
-      else if (c4 <= 256) e = launch_row_facts<4>(x, sl, prep, rows, B, (int)C, xstride, blank, s);
-      else if (c4 <= 512) e = launch_row_facts<8>(x, sl, prep, rows, B, (int)C, xstride, blank, s);
-      else if (c4 <= 768) e = launch_row_facts<12>(x, sl, prep, rows, B, (int)C, xstride, blank, s);
-      else if (c4 <= 1024) e = launch_row_facts<16>(x, sl, prep, rows, B, (int)C, xstride, blank, s);
-      else if (c4 <= 1280) e = launch_row_facts<20>(x, sl, prep, rows, B, (int)C, xstride, blank, s);
-      else if (c4 <= 1536) e = launch_row_facts<24>(x, sl, prep, rows, B, (int)C, xstride, blank, s);
-      else e = launch_row_facts<32>(x, sl, prep, rows, B, (int)C, xstride, blank, s);
-      if (e != hipSuccess) return e;
-      hipLaunchKernelGGL(ctcx_row_norm<T>, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, s, x, sl, norm, T_, B,
-                         C, xstride, (const char*)prep);
+#define CTCX_FACTS(NV) launch_row_facts<NV>(x, sl, prep, nf, rows, B, (int)C, xstride, blank, fuse, s)
+      if (c4 <= 64) e = CTCX_FACTS(1);
+      else if (c4 <= 128) e = CTCX_FACTS(2);
+      else if (c4 <= 256) e = CTCX_FACTS(4);
+      else if (c4 <= 512) e = CTCX_FACTS(8);
+      else if (c4 <= 768) e = CTCX_FACTS(12);
+      else if (c4 <= 1024) e = CTCX_FACTS(16);
+      else if (c4 <= 1280) e = CTCX_FACTS(20);
+      else if (c4 <= 1536) e = CTCX_FACTS(24);
+      else e = CTCX_FACTS(32);
+#undef CTCX_FACTS
+      if (e != hipSuccess || fuse) return e;
+      if (norm_v4())
+        hipLaunchKernelGGL(ctcx_row_norm_v4<>, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, s, x, sl, nf, T_, B,
+                           C, xstride, (const char*)prep);
+      else
+        hipLaunchKernelGGL(ctcx_row_norm<T>, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, s, x, sl, norm, T_, B,
+                           C, xstride, (const char*)prep);
       return hipGetLastError();
     }
   }

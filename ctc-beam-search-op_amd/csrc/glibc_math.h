@@ -108,6 +108,31 @@ template <class P>
 CTCX_HD float expf_t(float x, P tab) {   // tab[i] == exp2f_tab(i), e.g. in LDS
   return expf_impl(x, [tab](int i) { return (uint64_t)tab[i]; });
 }
+// expf_t for x <= 0, -inf or NaN (a softmax term x_j - max), without branches:
+// below -0x1.9fe368p6 (and at -inf) glibc returns 0, a NaN comes back as
+// x + x, and every other x <= 0 takes expf_impl's core path (from -88 down
+// to the underflow bound glibc falls through to it too); no overflow above.
+template <class P>
+CTCX_HD float expf_t_nonpos(float x, P tab) {
+  const bool under = x < -0x1.9fe368p6f;
+  const double xd = (double)(under ? 0.0f : x);   // (the core path's result is dropped then)
+  const double InvLn2N = 0x1.71547652b82fep+5;
+  const double Shift = 0x1.8p+52;
+  double kd = __builtin_fma(InvLn2N, xd, Shift);
+  const uint64_t ki = d2u(kd);
+  kd -= Shift;
+  const double r = __builtin_fma(InvLn2N, xd, -kd);
+  uint64_t t = (uint64_t)tab[(int)(ki % 32)];
+  t += ki << 47;
+  const double s = u2d(t);
+  const double zc = __builtin_fma(0x1.c6af84b912394p-20, r, 0x1.ebfce50fac4f3p-13);
+  const double r2 = r * r;
+  double y = __builtin_fma(0x1.62e42ff0c52d6p-6, r, 1.0);
+  y = __builtin_fma(zc, r2, y);
+  y = y * s;
+  const float e = under ? 0.0f : (float)y;
+  return x != x ? x + x : e;
+}
 
 // ---- logf ------------------------------------------------------------------
 CTCX_HD void logf_tab(int i, double& invc, double& logc) {

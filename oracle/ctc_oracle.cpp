@@ -77,6 +77,17 @@ inline double NumExp(double x) { return exp(x); }
 inline float NumLog(float x) { return logf(x); }
 inline double NumLog(double x) { return log(x); }
 
+// The softmax normaliser of one row (ctc_ext_beam_search_decoder.h:72-80):
+// maxCoeff's loop, the sum of exp(x_j - max) in class order, max + log(sum).
+template <typename T>
+T row_normaliser(const T* x, int64_t C) {
+  T mx = x[0];
+  for (int64_t j = 1; j < C; ++j) mx = std::max(mx, x[j]);
+  T s = T(0);
+  for (int64_t j = 0; j < C; ++j) s += NumExp(x[j] - mx);
+  return mx + NumLog(s);
+}
+
 // ---------------------------------------------------------------------------
 // gtl::TopN restatement.
 template <class E, class Greater>
@@ -295,12 +306,7 @@ class Decoder {
 
   // ctc_ext_beam_search_decoder.h:69-210
   void step(const T* x) {
-    T mx = x[0];
-    for (int j = 1; j < C_; ++j) mx = std::max(mx, x[j]);
-    T s = T(0);
-    for (int j = 0; j < C_; ++j) s += NumExp(x[j] - mx);
-    s = NumLog(s);
-    const T norm = mx + s;
+    const T norm = row_normaliser(x, C_);
 
     std::vector<N*> branches = leaves_.extract();
     leaves_.reset();
@@ -645,6 +651,14 @@ OracleResult* oracle_decode(int dtype, int mode, const void* x, const int32_t* s
                             int64_t T, int64_t B, int64_t C, int W, int P, int merge,
                             int blank_index, int blank_label) {
   return oracle_decode_scored(dtype, mode, x, seq_len, T, B, C, W, P, merge, blank_index, blank_label, nullptr);
+}
+
+// the normaliser of each of rows consecutive rows of C values (dtype as above)
+void oracle_row_norm(int dtype, const void* x, int64_t rows, int64_t C, void* out) {
+  for (int64_t r = 0; r < rows; ++r) {
+    if (dtype == 0) ((float*)out)[r] = oracle::row_normaliser((const float*)x + r * C, C);
+    else ((double*)out)[r] = oracle::row_normaliser((const double*)x + r * C, C);
+  }
 }
 
 void oracle_free(OracleResult* r) {

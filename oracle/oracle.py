@@ -65,8 +65,22 @@ def _load():
         lib.oracle_decode_ex.restype = ctypes.POINTER(_Result)
         lib.oracle_decode_ex.argtypes = lib.oracle_decode_scored.argtypes + [ctypes.c_int, ctypes.c_int64]
         lib.oracle_free.argtypes = [ctypes.POINTER(_Result)]
+        lib.oracle_row_norm.restype = None
+        lib.oracle_row_norm.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                        ctypes.c_void_p]
         _lib = lib
     return _lib
+
+
+def row_norm(rows):
+    """The softmax normaliser of each row of a [rows, C] float32/float64 array
+    (ctc_ext_beam_search_decoder.h:72-80, ctc_oracle.cpp row_normaliser)."""
+    x = np.ascontiguousarray(rows)
+    assert x.ndim == 2 and x.dtype in (np.float32, np.float64)
+    out = np.empty(x.shape[0], x.dtype)
+    _load().oracle_row_norm(0 if x.dtype == np.float32 else 1, x.ctypes.data, x.shape[0], x.shape[1],
+                            out.ctypes.data)
+    return out
 
 
 def raw_decode(inputs, sequence_length, beam_width, top_paths, merge_repeated=False,

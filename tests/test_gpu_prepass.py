@@ -8,8 +8,10 @@ labels than the set holds, the blank anywhere, C just above 64 up to 8196,
 and both the register path (float, C % 4 == 0: ctcx_row_facts) and the LDS
 path (ctcx_row_prep).  The decode parity tests cover the same records only
 through their effect on results; S is the gather's exactness bound
-(DESIGN.md "Kernels"), so it is pinned here directly.  The normaliser is
-covered by the decode parity tests (bit-exact log-probabilities)."""
+(DESIGN.md "Kernels"), so it is pinned here directly.  The normaliser the
+same launch writes (fused into ctcx_row_facts on the register path) is
+checked bit-exact against the oracle's (oracle.row_norm, decoder.h:72-80),
+NaN / +inf rows included, and rows past an item's length are left alone."""
 import ctypes
 import os
 import sys
@@ -19,6 +21,8 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "ctc-beam-search-op_amd"))
+
+import oracle  # noqa: E402  (tests/conftest.py puts oracle/ on the path)
 
 pytestmark = pytest.mark.gpu
 
@@ -75,7 +79,7 @@ def _rows(rng, C, kind, n):
     return x
 
 
-def _run(x_tb, C, blank, dtype=np.float32):
+def _run(x_tb, C, blank, dtype=np.float32, seq_len=None):
     import torch
     import ctcext_amd
     from ctcext_amd import _lib
@@ -85,10 +89,12 @@ def _run(x_tb, C, blank, dtype=np.float32):
     rb = ctypes.c_int64()
     dt = _lib.CTCEXT_F64 if dtype == np.float64 else _lib.CTCEXT_F32
     xs = torch.as_tensor(np.ascontiguousarray(x_tb.astype(dtype)), device="cuda")
-    sl = torch.full((B,), T, dtype=torch.int32, device="cuda")
+    if seq_len is None:
+        seq_len = np.full(B, T, np.int32)
+    sl = torch.as_tensor(np.asarray(seq_len, np.int32), device="cuda")
     assert lib.ctcext_row_facts(d.handle, None, dt, T, B, C, blank, None, None, None, ctypes.byref(rb)) == 0
     prep = torch.zeros(T * B * rb.value, dtype=torch.uint8, device="cuda")
-    norm = torch.zeros(T * B, dtype=torch.float64 if dtype == np.float64 else torch.float32, device="cuda")
+    norm = torch.full((T * B,), 7.5, dtype=torch.float64 if dtype == np.float64 else torch.float32, device="cuda")
     rc = lib.ctcext_row_facts(d.handle, ctypes.c_void_p(xs.data_ptr()), dt, T, B, C, blank,
                               ctypes.c_void_p(sl.data_ptr()), ctypes.c_void_p(prep.data_ptr()),
                               ctypes.c_void_p(norm.data_ptr()), ctypes.byref(rb))
@@ -96,12 +102,28 @@ def _run(x_tb, C, blank, dtype=np.float32):
     return prep.cpu().numpy().reshape(T * B, rb.value), norm.cpu().numpy()
 
 
-def _check_f32(x_tb, C, blank):
-    rec, _ = _run(x_tb, C, blank)
+def _check_norm(x_tb, norm, seq_len=None):
+    T, B, C = x_tb.shape
+    want = oracle.row_norm(x_tb.reshape(-1, C))
+    live = np.ones((T, B), bool) if seq_len is None else np.arange(T)[:, None] < np.asarray(seq_len)[None, :]
+    live = live.reshape(-1)
+    got = norm
+    same = (got.view(np.uint32 if got.dtype == np.float32 else np.uint64)
+            == want.view(np.uint32 if want.dtype == np.float32 else np.uint64)) | (np.isnan(got) & np.isnan(want))
+    assert same[live].all(), (C, np.flatnonzero(live & ~same)[:8], got[live & ~same][:4], want[live & ~same][:4])
+    assert (got[~live] == 7.5).all(), "rows past an item's length are not written"
+
+
+def _check_f32(x_tb, C, blank, seq_len=None):
+    rec, norm = _run(x_tb, C, blank, seq_len=seq_len)
+    _check_norm(x_tb, norm, seq_len)
     rows = x_tb.reshape(-1, C)
     nblk = (C + 63) // 64
     top_off = 16 + ((nblk * 4 + 15) & ~15)
+    live = None if seq_len is None else (np.arange(x_tb.shape[0])[:, None] < np.asarray(seq_len)[None, :]).reshape(-1)
     for r in range(rows.shape[0]):
+        if live is not None and not live[r]:
+            continue
         xmax, bad, bmax, sb, sl_, xout = _ref(rows[r], blank)
         h = rec[r]
         gmax = h[0:4].view(np.float32)[0]
@@ -130,12 +152,25 @@ def test_row_facts_match_definition(C):
             _check_f32(x, C, blank)
 
 
+@pytest.mark.parametrize("C", [68, 1000, 5000, 5001])
+def test_row_facts_ragged_lengths(C):
+    # items of different lengths: some of a block's four rows are past their
+    # item's end (the fused kernel's waves still meet its barriers)
+    rng = np.random.default_rng(7100 + C)
+    T, B = 5, 7
+    x = rng.standard_normal((T, B, C)).astype(np.float32) * 3
+    x[2, 3, C // 5] = np.nan
+    x[4, 0, 1] = np.inf
+    _check_f32(x, C, 0, seq_len=[5, 1, 0, 3, 4, 2, 5])
+
+
 def test_row_facts_f64_header_and_block_maxima():
     # double rows carry no top set (|S| = 0: the decode takes the plain path)
     C = 300
     rng = np.random.default_rng(7300)
     x = rng.standard_normal((2, 3, C))
-    rec, _ = _run(x, C, 5, np.float64)
+    rec, norm = _run(x, C, 5, np.float64)
+    _check_norm(x, norm)
     rows = x.reshape(-1, C)
     nblk = (C + 63) // 64
     for r in range(rows.shape[0]):
