@@ -4741,6 +4741,9 @@ __global__ __launch_bounds__(64) void ctcx_row_norm_v4(const float* __restrict__
     if (!h.bad) { m = h.xmax; known = true; }
   }
   const bool pass0 = __ballot(valid && !known) != 0ull;
+  // every row of the wave with its maximum from the header and finite (no
+  // NaN / +inf in the row, not all -inf): no term is NaN, expf_t_le0 serves
+  const bool le0 = __ballot(valid && !(known && m > -__builtin_inff())) == 0ull;
   // load q covers tile rows 8 q + sub, classes c4 .. c4 + 3 of the tile
   const int sub = lane >> 3, c4 = (lane & 7) * 4;
   const float* base[8];
@@ -4778,20 +4781,24 @@ __global__ __launch_bounds__(64) void ctcx_row_norm_v4(const float* __restrict__
           }
         } else if (nc == kNormTile) {
           // a whole tile: 16 exp terms in flight at a time, the sum in class order
+          auto tile_sum = [&](auto expf_fn) __attribute__((always_inline)) {
 #pragma unroll
-          for (int j0 = 0; j0 < kNormTile; j0 += 16) {
-            float e[16];
+            for (int j0 = 0; j0 < kNormTile; j0 += 16) {
+              float e[16];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const float4 w = *(const float4*)&tile[lane][j0 + 4 * i];
-              e[4 * i + 0] = gm::expf_t_nonpos(w.x - m, etab);
-              e[4 * i + 1] = gm::expf_t_nonpos(w.y - m, etab);
-              e[4 * i + 2] = gm::expf_t_nonpos(w.z - m, etab);
-              e[4 * i + 3] = gm::expf_t_nonpos(w.w - m, etab);
+              for (int i = 0; i < 4; ++i) {
+                const float4 w = *(const float4*)&tile[lane][j0 + 4 * i];
+                e[4 * i + 0] = expf_fn(w.x - m);
+                e[4 * i + 1] = expf_fn(w.y - m);
+                e[4 * i + 2] = expf_fn(w.z - m);
+                e[4 * i + 3] = expf_fn(w.w - m);
+              }
+#pragma unroll
+              for (int j = 0; j < 16; ++j) s += e[j];
             }
-#pragma unroll
-            for (int j = 0; j < 16; ++j) s += e[j];
-          }
+          };
+          if (le0) tile_sum([&](float v) __attribute__((always_inline)) { return gm::expf_t_le0(v, etab); });
+          else tile_sum([&](float v) __attribute__((always_inline)) { return gm::expf_t_nonpos(v, etab); });
         } else {
           for (int j = 0; j < nc; ++j) s += gm::expf_t_nonpos(tile[lane][j] - m, etab);
         }
@@ -5385,12 +5392,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_
     __syncthreads();   // the compact lists are done; etab, rmax and rsum are visible
     float s = 0.f;
     // the terms of tile u of row r, in place of its keys
+    // (a finite maximum: no term is NaN, expf_t_le0 serves; an all -inf row:
+    // every term NaN, as the reference's)
     auto terms = [&](const int r, const int u) __attribute__((always_inline)) {
       const bool inrow = 64 * u + lane < C4;
+      const bool fin = rxmax[r] > -__builtin_inff();   // wave-uniform
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const float v = (256 * u + c == bl4) ? xbv[r] : __uint_as_float(unkey(kr[r][u][c]));
-        kr[r][u][c] = __float_as_uint(inrow ? gm::expf_t_nonpos(v - rxmax[r], etab) : 0.f);
+        const float e = fin ? gm::expf_t_le0(v - rxmax[r], etab) : gm::expf_t_nonpos(v - rxmax[r], etab);
+        kr[r][u][c] = __float_as_uint(inrow ? e : 0.f);
       }
     };
     // row lane's 256 terms of one tile in class order (zeros past the row add

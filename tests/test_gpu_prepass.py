@@ -72,6 +72,10 @@ def _rows(rng, C, kind, n):
         x[:, : C // 7] = rng.standard_normal((n, C // 7)).astype(np.float32)
     elif kind == "flat":
         x[:] = np.float32(1.25)
+    elif kind == "all_neg_inf":  # a row of -inf only: maximum -inf, every term NaN
+        x[0, :] = -np.inf
+        if n > 2:
+            x[2, : C // 2] = -np.inf
     elif kind == "bad":
         x[0, C // 3] = np.nan
         if n > 1:
@@ -146,7 +150,7 @@ def _check_f32(x_tb, C, blank, seq_len=None):
 @pytest.mark.parametrize("C", [68, 256, 260, 1000, 2048, 5000, 8196, 65, 1001, 5001])
 def test_row_facts_match_definition(C):
     rng = np.random.default_rng(7000 + C)
-    for kind in ("normal", "ties", "neg_inf", "few_finite", "zeros", "flat", "bad"):
+    for kind in ("normal", "ties", "neg_inf", "few_finite", "zeros", "flat", "all_neg_inf", "bad"):
         for blank in (0, C - 1, C // 2):
             x = _rows(rng, C, kind, 6).reshape(2, 3, C)
             _check_f32(x, C, blank)

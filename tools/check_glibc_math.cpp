@@ -1,6 +1,7 @@
 // Exhaustive check: ctcx::gm::{expf,logf,log1pf} vs the host glibc libm over
-// every 32-bit float pattern, and gm::expf_t_nonpos (the fused normaliser's
-// branch-free expf) over every x <= 0, -inf and NaN.  Built with hipcc (host pass only) and
+// every 32-bit float pattern, gm::expf_t_nonpos (the normalisers' branch-free
+// expf) over every x <= 0, -inf and NaN, and gm::expf_t_le0 over every x <= 0
+// and -inf.  Built with hipcc (host pass only) and
 // -ffp-contract=off, exactly like the device code.
 //
 //   hipcc -O2 -ffp-contract=off -std=c++17 tools/check_glibc_math.cpp -o /tmp/chk -lpthread
@@ -48,6 +49,10 @@ int main(int argc, char** argv) {
         if (x <= 0.0f || x != x) {
           const float g3 = ctcx::gm::expf_t_nonpos(x, tab);
           if (!same(r0, g3)) { if (nb[3]++ < 4) printf("expf_t_nonpos %a: libm %a ours %a\n", x, r0, g3); }
+        }
+        if (x <= 0.0f) {   // (NaN excluded: expf_t_le0's domain)
+          const float g4 = ctcx::gm::expf_t_le0(x, tab);
+          if (!same(r0, g4)) { if (nb[3]++ < 4) printf("expf_t_le0 %a: libm %a ours %a\n", x, r0, g4); }
         }
       }
       for (int k = 0; k < 4; ++k) bad[k] += nb[k];
