@@ -139,6 +139,36 @@ __device__ __forceinline__ float wave_max_dpp(float v) {
   return ab > cd ? ab : cd;
 }
 __device__ __forceinline__ double wave_max_dpp(double v) { return wave_max(v); }
+// The maximum over each 16-lane DPP row, landing on the row's lane 15, by
+// v_max_f32_dpp (row_shr 1, 2, 4, 8; a lane without a source keeps its own
+// value); v must not be NaN.  As asm: the compiler's form moves the shifted
+// value, canonicalizes it and then takes the max (four instructions a step).
+// s_nop 1: a VGPR written by a VALU is read by a DPP two states later.
+__device__ __forceinline__ float row16_fmax_dpp(float v) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_max_f32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_max_f32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_max_f32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_max_f32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf"
+      : "+v"(v));
+  return v;
+}
+// the same by v_max_f32 (IEEE maxNum: a NaN operand loses; of +0 and -0
+// either may come back) -- for maxima whose zero sign nothing reads (the row
+// facts' maxima: compared, or subtracted from values as a softmax maximum)
+__device__ __forceinline__ float wave_fmax_dpp(float v) {
+  const float I = -__builtin_inff();
+  v = __builtin_fmaxf(v, dpp_f<0x111>(v, I));   // row_shr:1
+  v = __builtin_fmaxf(v, dpp_f<0x112>(v, I));   // row_shr:2
+  v = __builtin_fmaxf(v, dpp_f<0x114>(v, I));   // row_shr:4
+  v = __builtin_fmaxf(v, dpp_f<0x118>(v, I));   // row_shr:8
+  const float a = bcast(v, 15), b = bcast(v, 31), c = bcast(v, 47), d = bcast(v, 63);
+  return __builtin_fmaxf(__builtin_fmaxf(a, b), __builtin_fmaxf(c, d));
+}
 __device__ __forceinline__ unsigned wave_min_dpp(unsigned v) {
   const int I = -1;   // 0xffffffff
   int x = (int)v, w;
@@ -4836,6 +4866,11 @@ __device__ __forceinline__ unsigned fkey(float v) {
   const unsigned u = __float_as_uint(v);
   return u ^ ((u >> 31) ? 0xFFFFFFFFu : 0x80000000u);
 }
+// fkey through the sign's arithmetic shift: u ^ (sx | 0x80000000), sx = 0 or ~0
+__device__ __forceinline__ unsigned fkey_sx(float v) {
+  const unsigned u = __float_as_uint(v);
+  return u ^ ((unsigned)((int)u >> 31) | 0x80000000u);
+}
 
 template <typename T, bool INLDS>
 __global__ __launch_bounds__(64) void ctcx_row_prep(const T* __restrict__ x, const int32_t* __restrict__ seq_len,
@@ -5229,25 +5264,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_
       for (int c = 0; c < 4; ++c) {
         const float v = inrow ? __uint_as_float(k[u][c]) : NI;
         bad |= (v != v) || (v == PI);
-        lm = v > lm ? v : lm;
+        // the maxima by v_max_f32 (a NaN loses, as in v > lm ? v : lm; of
+        // +0 / -0 either: nothing reads a maximum's zero sign)
+        lm = __builtin_fmaxf(lm, v);
         // class 4 lane + 256 u + c is the blank iff 256 u + c == bl4 (no class
         // index per element: kept for the compaction, 80 of them took 80 VGPRs);
         // bitwise &: no short-circuit branch, so the key takes the value's register
-        const unsigned kv = fkey(v);
+        const unsigned kv = fkey_sx(v);
         k[u][c] = (inrow & (256 * u + c != bl4)) ? kv : 0u;
         lk = k[u][c] > lk ? k[u][c] : lk;
       }
-      xmax = lm > xmax ? lm : xmax;
-      float w;
-      w = dpp_f<0x111>(lm, NI); lm = w > lm ? w : lm;
-      w = dpp_f<0x112>(lm, NI); lm = w > lm ? w : lm;
-      w = dpp_f<0x114>(lm, NI); lm = w > lm ? w : lm;
-      w = dpp_f<0x118>(lm, NI); lm = w > lm ? w : lm;
+      xmax = __builtin_fmaxf(xmax, lm);
+      lm = row16_fmax_dpp(lm);
       const int kb = 4 * u + (lane >> 4);
       if ((lane & 15) == 15 && 64 * u < C4 && kb < nblk) bm[kb] = lm;
     }
     RowHdr<float> h;
-    h.xmax = wave_max_dpp(xmax);
+    h.xmax = wave_fmax_dpp(xmax);
     h.bad = __ballot(bad) != 0ull;
     const int K = kTopK;
     auto unkey = [](unsigned kv) { return kv ^ ((kv >> 31) ? 0x80000000u : 0xFFFFFFFFu); };   // fkey's inverse
