@@ -5156,8 +5156,9 @@ __device__ __forceinline__ unsigned radix_select_desc(const unsigned* cks, int n
 // already hold, so the logits are read from HBM once (ctcx_row_norm's second
 // read goes).  The sum stays in class order, one lane per row: after the
 // facts, the block's rows (two per wave) pass through LDS 256 classes at a
-// time as exp terms (two tile buffers over the compact lists, which are done
-// by then), lane q of wave 0 adding row q's tile in class order while the
+// time as exp terms (two tile buffers; these rows bisect their top set in
+// registers, with no compact list), lane q of wave 0 adding row q's tile in
+// class order while the
 // waves write the next one.  A row holding a NaN or +inf (max then in class
 // order) is summed from global memory by its wave's lane 0.  That chain, C
 // dependent adds per block, is the fused kernel's cost: the launcher fuses
@@ -5189,10 +5190,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_
   constexpr bool kRadix = NV > 4;
   constexpr int R = facts_rows_per_wave<NV, FUSE>();
   constexpr int NR = 4 * R;   // rows per block: row r * 4 + wave of the block's
-  constexpr int kCks = kRadix ? kFactsCompact + 64 : (FUSE ? 2 * R * kNormTileW : 1);
-  static_assert(!FUSE || 4 * kCks >= 2 * NR * kNormTileW, "the tile buffers fit over the compact lists");
-  __shared__ __attribute__((aligned(16))) unsigned cks_all[4][kCks];
-  __shared__ unsigned cls_all[4][kRadix ? kFactsCompact + 64 : 1];
+  constexpr int kCks = FUSE ? 2 * R * kNormTileW : 1;
+  static_assert(!FUSE || 4 * kCks >= 2 * NR * kNormTileW, "the tile buffers fit");
+  static_assert(!(FUSE && kRadix), "the normaliser is fused for NV <= 4 only (kFuseNorm)");
+  __shared__ __attribute__((aligned(16))) unsigned cks_all[4][kCks];   // FUSE: the tile buffers
+  // the compact list: a key plane and a label-index plane a constant
+  // 17 x 256 B apart, so each pair of stores is one ds_write2st64_b32
+  constexpr int kList = kRadix ? kFactsCompact + 64 : 1;
+  static_assert(!kRadix || (kList * 4) % 256 == 0, "planes 256-byte multiples apart");
+  __shared__ unsigned ckl_all[4][2][kList];
   __shared__ unsigned hist_all[4][kRadix ? 256 : 1];
   __shared__ uint64_t etab[FUSE ? 32 : 1];   // expf's table (read after the first tile barrier)
   __shared__ float rmax[FUSE ? NR : 1];   // the rows' maxima, for the summing lanes
@@ -5295,8 +5301,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_
     const unsigned kt = km > 1u ? km : 1u;
     // every key >= kt into the compact list, in label order (within a u, label
     // order is (lane, c) order): a label's slot is the count before it
-    unsigned* cks = cks_all[wv];
-    unsigned* cls = cls_all[wv];
+    unsigned* cks = ckl_all[wv][0];   // keys; labels at cks[kList + j]
     int n = 0;   // keys >= kt
     int lb4;   // 4 lane, opaque: recomputed here, not kept from the first pass
     __asm__ volatile("v_lshlrev_b32 %0, 2, %1" : "=v"(lb4) : "v"(lane));
@@ -5318,7 +5323,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_
           // label index: class 4 lane + 256 u + c, less one past the blank
           const int j = (in[c] && at < kFactsCompact) ? at : kFactsCompact + lane;
           cks[j] = k[u][c];
-          cls[j] = (unsigned)(lb4 + (256 * u + c) - (256 * u + c > bl4 ? 1 : 0));
+          cks[kList + j] = (unsigned)(lb4 + (256 * u + c) - (256 * u + c > bl4 ? 1 : 0));
           at += in[c] ? 1 : 0;
         }
 #pragma unroll
@@ -5341,7 +5346,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_
         const uint64_t mm = __ballot(in);
         if (in) {
           const int r = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mm, 0u));
-          top[ns + r] = make_uint2(unkey(kv), cls[j]);
+          top[ns + r] = make_uint2(unkey(kv), cks[kList + j]);
         }
         ns += __builtin_popcountll(mm);
       }
@@ -5422,7 +5427,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_
     }
     float* const tiles = (float*)&cks_all[0][0];   // [2][NR][kNormTileW]
     const int bl4 = blank - 4 * lane;
-    __syncthreads();   // the compact lists are done; etab, rmax and rsum are visible
+    __syncthreads();   // etab, rmax and rsum are visible
     float s = 0.f;
     // the terms of tile u of row r, in place of its keys
     // (a finite maximum: no term is NaN, expf_t_le0 serves; an all -inf row:
