@@ -5265,21 +5265,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_
 #pragma unroll
     for (int u = 0; u < NV; ++u) {
       float lm = NI;
-      const bool inrow = 64 * u + lane < C4;
+      // (a u wholly inside the row, the common case: no per-element row test)
+      auto keys = [&](auto whole) __attribute__((always_inline)) {
+        const bool inrow = decltype(whole)::value || 64 * u + lane < C4;
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const float v = inrow ? __uint_as_float(k[u][c]) : NI;
-        bad |= (v != v) || (v == PI);
-        // the maxima by v_max_f32 (a NaN loses, as in v > lm ? v : lm; of
-        // +0 / -0 either: nothing reads a maximum's zero sign)
-        lm = __builtin_fmaxf(lm, v);
-        // class 4 lane + 256 u + c is the blank iff 256 u + c == bl4 (no class
-        // index per element: kept for the compaction, 80 of them took 80 VGPRs);
-        // bitwise &: no short-circuit branch, so the key takes the value's register
-        const unsigned kv = fkey_sx(v);
-        k[u][c] = (inrow & (256 * u + c != bl4)) ? kv : 0u;
-        lk = k[u][c] > lk ? k[u][c] : lk;
-      }
+        for (int c = 0; c < 4; ++c) {
+          const float v = inrow ? __uint_as_float(k[u][c]) : NI;
+          bad |= (v != v) || (v == PI);
+          // the maxima by v_max_f32 (a NaN loses, as in v > lm ? v : lm; of
+          // +0 / -0 either: nothing reads a maximum's zero sign)
+          lm = __builtin_fmaxf(lm, v);
+          // class 4 lane + 256 u + c is the blank iff 256 u + c == bl4 (no class
+          // index per element: kept for the compaction, 80 of them took 80 VGPRs);
+          // bitwise &: no short-circuit branch, so the key takes the value's register
+          const unsigned kv = fkey_sx(v);
+          k[u][c] = (inrow & (256 * u + c != bl4)) ? kv : 0u;
+          lk = k[u][c] > lk ? k[u][c] : lk;
+        }
+      };
+      if (64 * u + 64 <= C4) keys(std::true_type{});   // uniform
+      else keys(std::false_type{});
       xmax = __builtin_fmaxf(xmax, lm);
       lm = row16_fmax_dpp(lm);
       const int kb = 4 * u + (lane >> 4);
@@ -5318,14 +5323,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_
           before += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mm[c] >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mm[c], 0u));
         }
         int at = n + before;
+        // (room for all of this u's 256 keys: no capacity test per key)
+        auto put = [&](auto room) __attribute__((always_inline)) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          // label index: class 4 lane + 256 u + c, less one past the blank
-          const int j = (in[c] && at < kFactsCompact) ? at : kFactsCompact + lane;
-          cks[j] = k[u][c];
-          cks[kList + j] = (unsigned)(lb4 + (256 * u + c) - (256 * u + c > bl4 ? 1 : 0));
-          at += in[c] ? 1 : 0;
-        }
+          for (int c = 0; c < 4; ++c) {
+            // label index: class 4 lane + 256 u + c, less one past the blank
+            const int j = (in[c] && (decltype(room)::value || at < kFactsCompact)) ? at : kFactsCompact + lane;
+            cks[j] = k[u][c];
+            cks[kList + j] = (unsigned)(lb4 + (256 * u + c) - (256 * u + c > bl4 ? 1 : 0));
+            at += in[c] ? 1 : 0;
+          }
+        };
+        if (n + 256 <= kFactsCompact) put(std::true_type{});   // uniform
+        else put(std::false_type{});
 #pragma unroll
         for (int c = 0; c < 4; ++c) n += __builtin_popcountll(mm[c]);
       }
