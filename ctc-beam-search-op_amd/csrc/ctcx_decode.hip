@@ -5275,12 +5275,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_
           // the maxima by v_max_f32 (a NaN loses, as in v > lm ? v : lm; of
           // +0 / -0 either: nothing reads a maximum's zero sign)
           lm = __builtin_fmaxf(lm, v);
-          // class 4 lane + 256 u + c is the blank iff 256 u + c == bl4 (no class
-          // index per element: kept for the compaction, 80 of them took 80 VGPRs);
-          // bitwise &: no short-circuit branch, so the key takes the value's register
+          // the blank's key is cleared below, in the one lane holding it
           const unsigned kv = fkey_sx(v);
-          k[u][c] = (inrow & (256 * u + c != bl4)) ? kv : 0u;
-          lk = k[u][c] > lk ? k[u][c] : lk;
+          k[u][c] = inrow ? kv : 0u;
         }
       };
       if (64 * u + 64 <= C4) keys(std::true_type{});   // uniform
@@ -5290,6 +5287,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_
       const int kb = 4 * u + (lane >> 4);
       if ((lane & 15) == 15 && 64 * u < C4 && kb < nblk) bm[kb] = lm;
     }
+    // the blank's key to 0 (it is no label): class 4 lane + 256 u + c, found
+    // by uniform tests on u and c and one lane select (not a compare per key)
+    {
+      const int ub = blank >> 8, cb = blank & 3, lbk = (blank >> 2) & 63;
+#pragma unroll
+      for (int u = 0; u < NV; ++u)
+        if (u == ub) {   // uniform
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            if (c == cb) k[u][c] = lane == lbk ? 0u : k[u][c];
+        }
+    }
+    auto umax = [](unsigned a, unsigned b) { return a > b ? a : b; };   // (pairs become v_max3_u32)
+#pragma unroll
+    for (int u = 0; u < NV; ++u) lk = umax(umax(lk, k[u][0]), umax(umax(k[u][1], k[u][2]), k[u][3]));
     RowHdr<float> h;
     h.xmax = wave_fmax_dpp(xmax);
     h.bad = __ballot(bad) != 0ull;
