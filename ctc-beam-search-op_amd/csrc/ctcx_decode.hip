@@ -5326,23 +5326,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_
     for (int u = 0; u < NV; ++u) {
       if (kRadix && 64 * u < C4) {   // uniform
         bool in[4];
-        int before = 0;
         uint64_t mm[4];
+        // the list slot of this lane's first key: n plus the keys in lower
+        // lanes, the four counts chained through mbcnt's accumulator
+        unsigned acc = (unsigned)n;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           in[c] = k[u][c] >= kt;
           mm[c] = __ballot(in[c]);
-          before += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mm[c] >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mm[c], 0u));
+          acc = __builtin_amdgcn_mbcnt_hi((unsigned)(mm[c] >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mm[c], acc));
         }
-        int at = n + before;
+        int at = (int)acc;
         // (room for all of this u's 256 keys: no capacity test per key)
         auto put = [&](auto room) __attribute__((always_inline)) {
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
-            // label index: class 4 lane + 256 u + c, less one past the blank
+            // the class (4 lane + 256 u + c); its label index (less one past
+            // the blank) is taken when S is written, not per key
             const int j = (in[c] && (decltype(room)::value || at < kFactsCompact)) ? at : kFactsCompact + lane;
             cks[j] = k[u][c];
-            cks[kList + j] = (unsigned)(lb4 + (256 * u + c) - (256 * u + c > bl4 ? 1 : 0));
+            cks[kList + j] = (unsigned)(lb4 + (256 * u + c));
             at += in[c] ? 1 : 0;
           }
         };
@@ -5368,7 +5371,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_
         const uint64_t mm = __ballot(in);
         if (in) {
           const int r = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mm, 0u));
-          top[ns + r] = make_uint2(unkey(kv), cks[kList + j]);
+          const unsigned cl = cks[kList + j];
+          top[ns + r] = make_uint2(unkey(kv), cl - (cl > (unsigned)blank ? 1u : 0u));
         }
         ns += __builtin_popcountll(mm);
       }
