@@ -137,6 +137,28 @@ CTCX_HD float expf_t_nonpos(float x, P tab) {
 // is finite and which holds no NaN / +inf): the core path runs on x as it is
 // (at -inf or below the underflow bound its result, garbage or NaN, is
 // dropped for glibc's 0), and no NaN select
+// expf's core path alone: glibc's expf for -0x1.9fe368p6 <= x <= 0 (a
+// caller that has checked the bound for a whole batch of terms)
+template <class P>
+CTCX_HD float expf_t_core(float x, P tab) {
+  const double xd = (double)x;
+  const double InvLn2N = 0x1.71547652b82fep+5;
+  const double Shift = 0x1.8p+52;
+  double kd = __builtin_fma(InvLn2N, xd, Shift);
+  const uint64_t ki = d2u(kd);
+  kd -= Shift;
+  const double r = __builtin_fma(InvLn2N, xd, -kd);
+  uint64_t t = (uint64_t)tab[(int)(ki % 32)];
+  t += ki << 47;
+  const double s = u2d(t);
+  const double zc = __builtin_fma(0x1.c6af84b912394p-20, r, 0x1.ebfce50fac4f3p-13);
+  const double r2 = r * r;
+  double y = __builtin_fma(0x1.62e42ff0c52d6p-6, r, 1.0);
+  y = __builtin_fma(zc, r2, y);
+  y = y * s;
+  return (float)y;
+}
+constexpr float kExpfUnder = -0x1.9fe368p6f;   // below it glibc's expf returns 0
 template <class P>
 CTCX_HD float expf_t_le0(float x, P tab) {
   const bool under = x < -0x1.9fe368p6f;

@@ -1,7 +1,7 @@
 // Exhaustive check: ctcx::gm::{expf,logf,log1pf} vs the host glibc libm over
 // every 32-bit float pattern, gm::expf_t_nonpos (the normalisers' branch-free
-// expf) over every x <= 0, -inf and NaN, and gm::expf_t_le0 over every x <= 0
-// and -inf.  Built with hipcc (host pass only) and
+// expf) over every x <= 0, -inf and NaN, gm::expf_t_le0 over every x <= 0
+// and -inf, and gm::expf_t_core over [the underflow bound, 0].  Built with hipcc (host pass only) and
 // -ffp-contract=off, exactly like the device code.
 //
 //   hipcc -O2 -ffp-contract=off -std=c++17 tools/check_glibc_math.cpp -o /tmp/chk -lpthread
@@ -53,6 +53,10 @@ int main(int argc, char** argv) {
         if (x <= 0.0f) {   // (NaN excluded: expf_t_le0's domain)
           const float g4 = ctcx::gm::expf_t_le0(x, tab);
           if (!same(r0, g4)) { if (nb[3]++ < 4) printf("expf_t_le0 %a: libm %a ours %a\n", x, r0, g4); }
+        }
+        if (x <= 0.0f && x >= ctcx::gm::kExpfUnder) {   // expf_t_core's domain
+          const float g5 = ctcx::gm::expf_t_core(x, tab);
+          if (!same(r0, g5)) { if (nb[3]++ < 4) printf("expf_t_core %a: libm %a ours %a\n", x, r0, g5); }
         }
       }
       for (int k = 0; k < 4; ++k) bad[k] += nb[k];
