@@ -5123,7 +5123,13 @@ __global__ __launch_bounds__(64) void ctcx_row_prep(const T* __restrict__ x, con
 #ifndef CTCX_FACTS_WPE
 #define CTCX_FACTS_WPE 1
 #endif
-constexpr int kFactsCompact = 1024;
+// (768: the block's lists in 30 KB, five blocks per CU -- cfg5's rows
+// gather ~270 keys; a row past it bisects instead.  1024 held four: c3k
+// 1.07 -> 0.98 ms, cfg5 7.09 -> 6.97 ms)
+#ifndef CTCX_FACTS_COMPACT
+#define CTCX_FACTS_COMPACT 768
+#endif
+constexpr int kFactsCompact = CTCX_FACTS_COMPACT;
 // The (rank)-th largest of the n keys of a wave's compact list (rank <= n):
 // MSB-first radix select, 8-bit digits, a 256-bin LDS histogram per pass.
 // Every key lies in [klo, khi], so the bits above their highest differing bit
