@@ -156,6 +156,18 @@ def test_row_facts_match_definition(C):
             _check_f32(x, C, blank)
 
 
+@pytest.mark.parametrize("C", [124, 128, 512, 516, 772, 1020, 1024, 1028, 2048, 3072])
+def test_row_facts_nv_boundaries(C):
+    # the row widths at the edges of each compiled NV (and of the fused
+    # normaliser's C <= 1024), 5 x 7 rows: the last block of eight (two rows
+    # per wave, fused) or four rows only partly filled
+    rng = np.random.default_rng(7200 + C)
+    x = (rng.standard_normal((5, 7, C)) * 2).astype(np.float32)
+    x[1, 2, :] = -np.inf
+    x[3, 4, C // 3] = np.nan
+    _check_f32(x, C, C // 5, seq_len=[5, 4, 5, 2, 5, 3, 1])
+
+
 @pytest.mark.parametrize("C", [68, 1000, 5000, 5001])
 def test_row_facts_ragged_lengths(C):
     # items of different lengths: some of a block's four rows are past their
