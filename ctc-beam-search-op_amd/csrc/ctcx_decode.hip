@@ -2273,6 +2273,71 @@ __device__ __forceinline__ void help_gather_scored(const Ctx<T>& cx, GQ q, int b
   if (BIG && cbr >= 0) cq_children(cx, buf, nb, cbr, -1);   // the child bitmap starts the next frame clear
 }
 
+// Extract by rank, beside wave 0's sort_heap (SQ kernels, beams <= 128).
+// sort_heap over a valid heap yields the totals in descending order; only the
+// order WITHIN a group of equal totals depends on the heap's shape.  So if
+// positions 0..p-1 hold entries whose totals are all distinct (p = the
+// smallest rank of any tied entry, rank = the number of larger totals), each
+// of them lands at its rank whatever the pops do, and wave 0 need only pop
+// positions W-1 down to p.  Wave 0 copies the final heap (totals to
+// cx.newpos, slots to cx.alias: neither is read between the grow and the
+// commit) and raises kCtlExt before kCtlDone; the helper ranks the copy,
+// writes sorted[r] for every r < p, then publishes p in kCtlStop.  Wave 0
+// never waits for it: it reads kCtlStop between extract segments and stops at
+// p once it sees one (round 3 placed by rank on wave 0: the rank pass cost
+// ~5k cycles per frame, about what it saved).  A position both write holds the
+// same slot either way.
+#ifndef CTCX_EXT_RANK
+#define CTCX_EXT_RANK 1
+#endif
+constexpr bool kExtRank = CTCX_EXT_RANK != 0;
+constexpr int kCtlStop = 3, kCtlExt = 7;   // (misc words; both reset per frame)
+constexpr int kExtMinW = 16;               // beams below this pop too few positions to gain
+template <typename T>
+__device__ __forceinline__ void help_rank_extract(const Ctx<T>& cx) {
+  const int lane = threadIdx.x & 63;
+  CTCX_LDS int* m = cx.misc;
+  if (ctl_ld(m, kCtlDead) != 0) return;
+  uint64_t tw = 0;
+  for (int spin = 0;; ++spin) {   // wave 0's grow over (its copy, if any, is then in place)
+    if (ctl_ld(m, kCtlDone) != 0) break;
+    if (wait_expired(spin, tw)) {
+      __hip_atomic_store(&m[kCtlDead], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(CTCX_SLEEP);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  if (ctl_ld(m, kCtlExt) != 1) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  const int W = cx.W;
+  const CTCX_LDS float* xv = (const CTCX_LDS float*)cx.newpos;
+  const bool in0 = lane < W, in1 = lane + 64 < W;
+  const float v0 = in0 ? xv[lane] : 0.0f, v1 = in1 ? xv[lane + 64] : 0.0f;
+  int g0 = 0, e0 = 0, g1 = 0, e1 = 0;
+  const int W4 = (W + 3) >> 2;   // (wave 0 pads the copy to a multiple of 4 with NaN: never > or ==)
+  for (int j = 0; j < W4; ++j) {
+    const u32x4 xq = ((const CTCX_LDS u32x4*)xv)[j];   // one address: a broadcast
+    const float x[4] = {__uint_as_float(xq.x), __uint_as_float(xq.y), __uint_as_float(xq.z), __uint_as_float(xq.w)};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      g0 += x[u] > v0;
+      e0 += x[u] == v0;
+      g1 += x[u] > v1;
+      e1 += x[u] == v1;
+    }
+  }
+  if (__ballot((in0 && v0 != v0) || (in1 && v1 != v1))) return;   // (no order to rank by)
+  int p = W;
+  if (in0 && e0 > 1) p = g0 < p ? g0 : p;
+  if (in1 && e1 > 1) p = g1 < p ? g1 : p;
+  p = uni(wave_min(p));
+  if (p <= 2) return;   // wave 0 pops every position anyway
+  if (in0 && g0 < p) cx.sorted[g0] = cx.alias[lane];
+  if (in1 && g1 < p) cx.sorted[g1] = cx.alias[lane + 64];
+  __hip_atomic_store(&m[kCtlStop], p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 template <typename T>
 __device__ __forceinline__ void help_gather_chunks(const Ctx<T>& cx, GQ q, int buf, int nb, T norm, T pmax, T bottom,
                                                    int lead) {
@@ -2382,6 +2447,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     if (helper_wave()) {
       if constexpr (SQ) {
         if (nb >= W) help_gather_scored<T, BIG>(cx, gq, buf, nb, norm, pmax, wave_min(lmin));
+        if constexpr (RN == 1 && kExtRank) help_rank_extract<T>(cx);
       } else if constexpr (BIG) {
         // how far ahead of wave 0 the helper gathers (at most kQSlots chunks):
         // a chunk gathered early carries offers a later bottom rejects, and at
@@ -3454,6 +3520,27 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     if (pc) pc[9] += __builtin_amdgcn_s_memtime() - tc1;
   }
 
+  // the extract's rank placement on the helper (help_rank_extract): the final
+  // heap's copy, then kCtlExt, both ahead of kCtlDone
+  const bool ext_rank = HW && SQ && RN == 1 && kExtRank && st == kTopHeap && W >= kExtMinW;
+  if constexpr (HW && SQ && RN == 1 && kExtRank) {
+    if (ext_rank) {
+      CTCX_LDS float* xv = (CTCX_LDS float*)cx.newpos;
+      const int W4 = (W + 3) & ~3;
+#pragma unroll
+      for (int k0 = 0; k0 < 128; k0 += 64) {
+        const int k = k0 + lane;
+        if (k < W) {
+          xv[k] = (float)he[k + 1].v;
+          cx.alias[k] = he[k + 1].s;
+        } else if (k < W4) {
+          xv[k] = __builtin_nanf("");
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // (one wave's LDS operations run in order)
+      if (lane == 0) __hip_atomic_store(&cx.misc[kCtlExt], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
   // the grow is over: the helper stops scoring
   if constexpr (HW) __hip_atomic_store(&cx.misc[kCtlDone], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   if (BIG && cbr >= 0) cq_children(cx, buf, nb, cbr, -1);
@@ -3483,14 +3570,33 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     const HeapM geo = heap_m(cx.hdum);
     int fs = front.s;
     int srt0 = 0, srt1 = 0;
+    int stop = 2;   // positions below it: placed by rank (help_rank_extract)
     if constexpr (sizeof(T) == 4) {
       const unsigned heb = (unsigned)(uintptr_t)he;
       const unsigned aj = heb + 8u * (unsigned)(lane + 1), al = heb + 8u * (unsigned)(2 * lane + 2);
       const unsigned ar = al + 8u, dum = heb + 8u * (unsigned)(cx.hdum + lane);
       fs = uni(fs);
-      // positions 127..64 into srt1, 63..2 into srt0
-      if (W > 64) extract_f32(heb, uni(W), 64, 64, geo.anc, geo.req, aj, al, ar, dum, srt1, fs);
-      extract_f32(heb, uni(W < 64 ? W : 64), 2, 0, geo.anc, geo.req, aj, al, ar, dum, srt0, fs);
+      // positions 127..64 into srt1, 63..2 into srt0, in four segments; with
+      // the helper ranking (ext_rank), kCtlStop is read between them and the
+      // pops end at the first position it has not placed
+      auto seg = [&](int top, int lo, int base, int& srt) {
+        const int hi = W < top ? W : top;
+        const int l = lo > stop ? lo : stop;
+        if (hi > l) extract_f32(heb, uni(hi), uni(l), base, geo.anc, geo.req, aj, al, ar, dum, srt, fs);
+      };
+      auto poll = [&]() {
+        if (ext_rank) {
+          const int p = ctl_ld(cx.misc, kCtlStop);
+          stop = p > stop ? p : stop;
+        }
+      };
+      seg(128, 96, 64, srt1);
+      poll();
+      seg(96, 64, 64, srt1);
+      poll();
+      seg(64, 32, 0, srt0);
+      poll();
+      seg(32, 2, 0, srt0);
     } else {
       for (int len = W; len > 2; --len) {
         const HE<T> v = he_ld(he, len);   // e[len-1] (uniform address)
@@ -3508,11 +3614,15 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       }
     }
     // pop_heap(2): the front goes to position 1, e[1] becomes the root
-    srt0 = writelane(srt0, fs, 1);
-    srt0 = writelane(srt0, uni(he_ld(he, 2).s), 0);
+    if (stop <= 2) {
+      srt0 = writelane(srt0, fs, 1);
+      srt0 = writelane(srt0, uni(he_ld(he, 2).s), 0);
+    }
     nout = W;
-    if (lane < nout) cx.sorted[lane] = srt0;
-    if (lane + 64 < nout) cx.sorted[lane + 64] = srt1;
+    // (positions below a stop the helper published: the helper's)
+    const int from = stop > 2 ? stop : 0;
+    if (lane < nout && lane >= from) cx.sorted[lane] = srt0;
+    if (lane + 64 < nout && lane + 64 >= from) cx.sorted[lane + 64] = srt1;
   } else if (RN == 2 && st == kTopHeap) {
     // sort_heap in the two-node mask form (beams 129..256), positions into
     // register lanes as above (position p: lane p & 63 of srt[p >> 6])
@@ -4293,6 +4403,8 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
     if constexpr (HW) {   // the helper's hand-over words, per frame
       if (tid < 3) cx.misc[kCtlReady + tid] = 0;
       if (tid == 3) cx.misc[kCtlBot] = (int)0xff800000u;   // -inf
+      if (tid == 4) cx.misc[kCtlExt] = 0;
+      if (tid == 5) cx.misc[kCtlStop] = 0;
     }
     const T norm = prm.norm[(int64_t)t * B + b];
     if constexpr (BIG) {
