@@ -2290,7 +2290,14 @@ __device__ __forceinline__ void help_gather_scored(const Ctx<T>& cx, GQ q, int b
 #ifndef CTCX_EXT_RANK
 #define CTCX_EXT_RANK 1
 #endif
+#ifndef CTCX_EXT_BIG
+#define CTCX_EXT_BIG 0
+#endif
+#ifndef CTCX_EXT_SLEEP
+#define CTCX_EXT_SLEEP 1
+#endif
 constexpr bool kExtRank = CTCX_EXT_RANK != 0;
+constexpr bool kExtBig = CTCX_EXT_BIG != 0;   // large C too: off (cfg4 162.5 -> 169.6 ms, same box; cfg3 unmoved)
 constexpr int kCtlStop = 3, kCtlExt = 7;   // (misc words; both reset per frame)
 constexpr int kExtMinW = 16;               // beams below this pop too few positions to gain
 template <typename T>
@@ -2305,7 +2312,7 @@ __device__ __forceinline__ void help_rank_extract(const Ctx<T>& cx) {
       __hip_atomic_store(&m[kCtlDead], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       return;
     }
-    __builtin_amdgcn_s_sleep(CTCX_SLEEP);
+    __builtin_amdgcn_s_sleep(CTCX_EXT_SLEEP);
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   if (ctl_ld(m, kCtlExt) != 1) return;
@@ -2447,7 +2454,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     if (helper_wave()) {
       if constexpr (SQ) {
         if (nb >= W) help_gather_scored<T, BIG>(cx, gq, buf, nb, norm, pmax, wave_min(lmin));
-        if constexpr (RN == 1 && kExtRank) help_rank_extract<T>(cx);
+        if constexpr (RN == 1 && kExtRank && (kExtBig || !BIG)) help_rank_extract<T>(cx);
       } else if constexpr (BIG) {
         // how far ahead of wave 0 the helper gathers (at most kQSlots chunks):
         // a chunk gathered early carries offers a later bottom rejects, and at
@@ -3522,8 +3529,9 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
 
   // the extract's rank placement on the helper (help_rank_extract): the final
   // heap's copy, then kCtlExt, both ahead of kCtlDone
-  const bool ext_rank = HW && SQ && RN == 1 && kExtRank && st == kTopHeap && W >= kExtMinW;
-  if constexpr (HW && SQ && RN == 1 && kExtRank) {
+  constexpr bool kExt = HW && SQ && RN == 1 && kExtRank && (kExtBig || !BIG);
+  const bool ext_rank = kExt && st == kTopHeap && W >= kExtMinW;
+  if constexpr (kExt) {
     if (ext_rank) {
       CTCX_LDS float* xv = (CTCX_LDS float*)cx.newpos;
       const int W4 = (W + 3) & ~3;
