@@ -2297,6 +2297,10 @@ __device__ __forceinline__ void help_gather_scored(const Ctx<T>& cx, GQ q, int b
 #define CTCX_EXT_SLEEP 1
 #endif
 constexpr bool kExtRank = CTCX_EXT_RANK != 0;
+#ifndef CTCX_EXT_LATE
+#define CTCX_EXT_LATE 0
+#endif
+constexpr bool kExtLate = CTCX_EXT_LATE != 0;   // (A/B: the helper ranks after its pending ring flush)
 constexpr bool kExtBig = CTCX_EXT_BIG != 0;   // large C too: off (cfg4 162.5 -> 169.6 ms, same box; cfg3 unmoved)
 constexpr int kCtlStop = 3, kCtlExt = 7;   // (misc words; both reset per frame)
 constexpr int kExtMinW = 16;               // beams below this pop too few positions to gain
@@ -2454,7 +2458,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     if (helper_wave()) {
       if constexpr (SQ) {
         if (nb >= W) help_gather_scored<T, BIG>(cx, gq, buf, nb, norm, pmax, wave_min(lmin));
-        if constexpr (RN == 1 && kExtRank && (kExtBig || !BIG)) help_rank_extract<T>(cx);
+        if constexpr (RN == 1 && kExtRank && (kExtBig || !BIG) && !kExtLate) help_rank_extract<T>(cx);
       } else if constexpr (BIG) {
         // how far ahead of wave 0 the helper gathers (at most kQSlots chunks):
         // a chunk gathered early carries offers a later bottom rejects, and at
@@ -4457,6 +4461,8 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
       }
       if (helper_wave() && pf_t >= 0)   // the helper: the flush the previous commit left pending
         ring_flush<(WC > 0 ? WC : 512) / 64, RT, true>(rg, rstream, foff, pf_t, pf_lo, pf_hi, nullptr, 0, pf_fp, nrec);
+      if constexpr (SQ && RN == 1 && kExtRank && (kExtBig || !BIG) && kExtLate)
+        if (helper_wave()) help_rank_extract<T>(cx);
       pf_t = -1;
       __syncthreads();
       why = uni(cx.misc[4]);
