@@ -268,8 +268,12 @@ extern "C" int ctcext_row_facts(ctcext_decoder* d, const void* x, int32_t dtype,
   return CTCEXT_OK;
 }
 
+// Frozen at the ABI-4 struct (every field before helper_redecodes): a binary
+// built against that header passes a struct of that size, and a copy of the
+// grown struct would write past it.  Fields added since are read through
+// ctcext_get_stats_sized only.
 extern "C" int ctcext_get_stats(ctcext_decoder* d, ctcext_stats* s) {
-  return ctcext_get_stats_sized(d, s, sizeof(ctcext_stats));
+  return ctcext_get_stats_sized(d, s, offsetof(ctcext_stats, helper_redecodes));
 }
 
 // The struct has grown by appending fields (ctcext.h); a caller built against
@@ -443,7 +447,10 @@ static int enqueue_shard(ctcext_decoder* d, Dev& v, bool root, const ctcext_deco
   p.seq_len = sl;
   p.Tmax = T_; p.B = Bs; p.C = C; p.xstride = xstride;
   p.W = W; p.P = P; p.blank = a->blank_index; p.blank_label = a->blank_label;
-  p.force_literal = (a->flags & CTCEXT_FLAG_FORCE_LITERAL) ? 1 : 0;
+  // num_classes == 1 (the blank alone): no label is ever offered, and the
+  // fast paths' offer arithmetic divides by C - 1, so every frame takes the
+  // literal path (the reference's own loops, decoder.h:146-209, then empty)
+  p.force_literal = ((a->flags & CTCEXT_FLAG_FORCE_LITERAL) || C < 2) ? 1 : 0;
   p.rec = (ctcx::Rec*)v.rec.p;
   p.item = (ctcx::ItemOut*)v.item.p;
   p.top_pos = (int32_t*)v.top_pos.p;

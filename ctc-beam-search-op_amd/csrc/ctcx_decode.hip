@@ -1690,6 +1690,27 @@ __device__ __forceinline__ Tab tab_carve(CTCX_LDS char* p) {
   t.p = (CTCX_LDS float*)(p + (size_t)kTabSlots * 64 * 16);
   return t;
 }
+// Per-phase cycle counters of the diagnostics build (CTCX_PHASES), one set per
+// item in HBM: wave 0's lane 0 adds each sample with a global atomic that
+// returns nothing (the wave never waits on it), so the counters cost the
+// decode no registers across its loops (round 5 kept 24 of them in SGPR
+// pairs, which moved the hot loops' register allocation and inflated the
+// "glue" they measured).  A null pointer compiles every use away.
+struct PhaseCtr {
+  uint64_t* p;
+  struct Ref {
+    uint64_t* a;
+    __device__ __forceinline__ void operator+=(uint64_t v) const {
+      if (threadIdx.x == 0) __hip_atomic_fetch_add(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __device__ __forceinline__ void operator=(uint64_t v) const {
+      if (threadIdx.x == 0) __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
+  __device__ __forceinline__ explicit operator bool() const { return p != nullptr; }
+  __device__ __forceinline__ Ref operator[](int i) const { return Ref{p + i}; }
+};
+
 // control words in misc[8..11]; kCtlDead (sticky for the kernel): a wait ran
 // out of time, every later wait returns at once, wave 0 ends every grow
 // without reading the table or queue, and the item reports it (ItemOut.pad)
@@ -1788,7 +1809,7 @@ __device__ __forceinline__ void help_score_chunks(const Ctx<T>& cx, Tab tb, int 
 template <typename T>
 __device__ __forceinline__ void gather_chunk(const Ctx<T>& cx, int buf, int nb, T norm, T pmax, T bottom, int tsn,
                                              T txo, int& i0, int& li0, int& cbr, bool& gstop,
-                                             CTCX_LDS uint32_t* cq, int& cqn, uint64_t* pc, int cap = 64) {
+                                             CTCX_LDS uint32_t* cq, int& cqn, PhaseCtr pc, int cap = 64) {
   const int lane = threadIdx.x & 63;
   const T NI = ninf<T>();
   const int Cm1 = cx.C - 1;
@@ -2233,7 +2254,7 @@ __device__ __forceinline__ void help_gather_scored(const Ctx<T>& cx, GQ q, int b
       // value word
       CTCX_LDS uint32_t* sc = (CTCX_LDS uint32_t*)qp;
       // (the frame's first chunk capped at kSqCap0 offers, so wave 0 starts sooner)
-      gather_chunk<T>(cx, buf, nb, norm, pmax, bottom, tsn, txo, i0, li0, cbr, gstop, sc, cqn, nullptr,
+      gather_chunk<T>(cx, buf, nb, norm, pmax, bottom, tsn, txo, i0, li0, cbr, gstop, sc, cqn, PhaseCtr{nullptr},
                       c == 0 ? kSqCap0 : 64);
       wsync<true>();
       const bool v = lane < cqn;
@@ -2379,7 +2400,7 @@ __device__ __forceinline__ void help_gather_chunks(const Ctx<T>& cx, GQ q, int b
     const int slot = c & q.sm;
     const int s_i0 = i0, s_l0 = li0;
     int cqn = 0;
-    gather_chunk<T>(cx, buf, nb, norm, pmax, bottom, tsn, txo, i0, li0, cbr, gstop, q.e + slot * 64, cqn, nullptr);
+    gather_chunk<T>(cx, buf, nb, norm, pmax, bottom, tsn, txo, i0, li0, cbr, gstop, q.e + slot * 64, cqn, PhaseCtr{nullptr});
     if (lane == 0) {
       q.h[slot * 4 + 0] = cqn;
       q.h[slot * 4 + 1] = s_i0;
@@ -2397,7 +2418,7 @@ __shared__ int g_sq_dbg[8];   // (diagnostics: the first scored-field mismatch)
 #endif
 template <typename T, int RN, bool BIG, class SC, bool HW, bool SQ>
 __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, bool last, int P, int* n_out,
-                          int* n_leaves, uint64_t* pc, Tab tb, GQ gq) {
+                          int* n_leaves, PhaseCtr pc, Tab tb, GQ gq) {
   // SQ: the scored gather queue (two-wave kernels, beams <= 128, any C): with
   // the beam full, every chunk of the grow comes from the helper scored
   static_assert(!SQ || (HW && (RN == 1 || (RN == 2 && BIG))), "SQ kernels");
@@ -3549,12 +3570,17 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
           xv[k] = __builtin_nanf("");
         }
       }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // (one wave's LDS operations run in order)
+      // release (LDS only: no wait on the record stores): the copy before kCtlExt
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
       if (lane == 0) __hip_atomic_store(&cx.misc[kCtlExt], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
-  // the grow is over: the helper stops scoring
-  if constexpr (HW) __hip_atomic_store(&cx.misc[kCtlDone], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  // the grow is over: the helper stops scoring.  Released (LDS only): the
+  // helper's acquire after it reads kCtlDone then sees kCtlExt and the copy
+  if constexpr (HW) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __hip_atomic_store(&cx.misc[kCtlDone], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
   if (BIG && cbr >= 0) cq_children(cx, buf, nb, cbr, -1);
   uint64_t ts2 = pc ? __builtin_amdgcn_s_memtime() : 0;
   if (pc) pc[2] += ts2 - ts1;
@@ -3597,8 +3623,8 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
         if (hi > l) extract_f32(heb, uni(hi), uni(l), base, geo.anc, geo.req, aj, al, ar, dum, srt, fs);
       };
       auto poll = [&]() {
-        if (ext_rank) {
-          const int p = ctl_ld(cx.misc, kCtlStop);
+        if (ext_rank) {   // acquire: the helper's sorted[] writes before its release of kCtlStop
+          const int p = uni(__hip_atomic_load(&cx.misc[kCtlStop], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
           stop = p > stop ? p : stop;
         }
       };
@@ -4369,12 +4395,13 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
   __syncthreads();
 
 #ifdef CTCX_PHASES
-  // per-phase s_memtime accumulators (diagnostics builds only: the 16 live
-  // 64-bit counters cost the hot loops SGPRs)
-  uint64_t pc[kPhaseN] = {};
+  // per-phase s_memtime accumulators (diagnostics builds only; PhaseCtr)
   const bool prof = prm.prof != nullptr;
+  const PhaseCtr pc{prof ? prm.prof + (size_t)b * kPhaseN : nullptr};
+  if (prof && tid == 0)
+    for (int q = 0; q < kPhaseN; ++q) pc.p[q] = 0;
 #else
-  uint64_t pc[kPhaseN];
+  const PhaseCtr pc{nullptr};
   constexpr bool prof = false;
 #endif
   for (int t = 0; t < sl; ++t) {
@@ -4448,7 +4475,7 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
     if (prof) pc[0] += t1 - t0;
 #ifndef CTCX_GSTATE   // the global-state tier replays every frame literally
     if (!prm.force_literal && !dup)
-      why = exact_step<T, RN, BIG, SC, HW, SQ>(cx, buf, nb, norm, last, prm.P, &n, &nl_fast, prof ? pc : nullptr, tb, gq);
+      why = exact_step<T, RN, BIG, SC, HW, SQ>(cx, buf, nb, norm, last, prm.P, &n, &nl_fast, prof ? pc : PhaseCtr{nullptr}, tb, gq);
 #endif
     if constexpr (HW) {
       // wave 0's result for both waves; the helper stops if the grow ended
@@ -4671,8 +4698,6 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
     if (prof) { pc[21] = (uint64_t)__builtin_amdgcn_s_getreg(63492); pc[22] = (uint64_t)(uint32_t)misc[14]; }
   }
 #endif
-  if (prof && tid == 0)
-    for (int q = 0; q < kPhaseN; ++q) prm.prof[b * kPhaseN + q] = pc[q];
 
   // TopPaths outputs (decoder.h:230-261); with no frames the root is the leaf
   if (sl == 0 && tid == 0) cx.tops[0] = 0;
@@ -5988,7 +6013,8 @@ static hipError_t launch_decode_r(const DecodeParams<T>& p, hipStream_t s) {
 // 2 only), kHelperScored (kind 3 where it applies).
 template <typename T>
 int helper_kind(const DecodeParams<T>& p, int mode) {
-  if (mode == kHelperNone || sizeof(T) != 4 || p.scorer_tab != nullptr) return 0;
+  // (C == 1: no label offers; the one-wave kernel's literal path, ctcext_capi)
+  if (mode == kHelperNone || sizeof(T) != 4 || p.scorer_tab != nullptr || p.C < 2) return 0;
   if ((mode == kHelperScored || mode == kHelperScoredWide) && p.C <= kSqMaxClasses &&
       (p.W <= 128 || (mode == kHelperScoredWide && p.W <= 256 && p.C > 64)))
     return 3;

@@ -133,10 +133,6 @@ CTCX_HD float expf_t_nonpos(float x, P tab) {
   const float e = under ? 0.0f : (float)y;
   return x != x ? x + x : e;
 }
-// expf_t_nonpos for x <= 0 or -inf, never NaN (a term of a row whose maximum
-// is finite and which holds no NaN / +inf): the core path runs on x as it is
-// (at -inf or below the underflow bound its result, garbage or NaN, is
-// dropped for glibc's 0), and no NaN select
 // expf's core path alone: glibc's expf for -0x1.9fe368p6 <= x <= 0 (a
 // caller that has checked the bound for a whole batch of terms)
 template <class P>
@@ -159,6 +155,10 @@ CTCX_HD float expf_t_core(float x, P tab) {
   return (float)y;
 }
 constexpr float kExpfUnder = -0x1.9fe368p6f;   // below it glibc's expf returns 0
+// expf_t_nonpos for x <= 0 or -inf, never NaN (a term of a row whose maximum
+// is finite and which holds no NaN / +inf): the core path runs on x as it is
+// (at -inf or below the underflow bound its result, garbage or NaN, is
+// dropped for glibc's 0), and no NaN select
 template <class P>
 CTCX_HD float expf_t_le0(float x, P tab) {
   const bool under = x < -0x1.9fe368p6f;

@@ -21,6 +21,7 @@ torch tensors.  Decoding always runs on the GPU through libctcext.so.
 import collections
 import ctypes
 import threading
+import warnings
 
 import numpy as np
 
@@ -117,6 +118,13 @@ class Decoder:
         if rc != _lib.CTCEXT_OK:
             _raise(self.lib, rc)
         self.last_stats = self.stats()
+        if self.last_stats.get("helper_redecodes", 0) > 0:
+            # a two-wave kernel's hand-over wait ran out of time (never in a
+            # correct run): the outputs are right, decoded again by the
+            # one-wave kernels, but the call took up to ~2x its time
+            warnings.warn("ctc_ext_beam_search_decoder: a helper-wave hand-over wait timed out; the call was "
+                          "decoded again with the one-wave kernels (ctcext_stats.helper_redecodes = %d)"
+                          % self.last_stats["helper_redecodes"], RuntimeWarning, stacklevel=3)
         return [(s.num_decoded, s.max_decoded, s.num_alignment, s.max_alignment) for s in sizes]
 
     # -- phase 2 ---------------------------------------------------------

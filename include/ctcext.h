@@ -186,9 +186,10 @@ int ctcext_decode_sharded(ctcext_decoder* dec, const ctcext_decode_args* args, c
 /* Phase 2 (StoreAllDecodedSequences + log_probability).  Synchronous. */
 int ctcext_fetch(ctcext_decoder* dec, const ctcext_outputs* out);
 
-/* Statistics of the last decode.  ctcext_get_stats fills this header's whole
- * struct; ctcext_get_stats_sized fills the first `size` bytes only (a caller
- * built against an older header passes its sizeof(ctcext_stats)). */
+/* Statistics of the last decode.  ctcext_get_stats fills the ABI-4 prefix
+ * only (every field before helper_redecodes: callers built against that
+ * header pass a struct of that size); ctcext_get_stats_sized fills the first
+ * `size` bytes (pass sizeof(ctcext_stats) for every field of this header). */
 int ctcext_get_stats(ctcext_decoder* dec, ctcext_stats* stats);
 int ctcext_get_stats_sized(ctcext_decoder* dec, ctcext_stats* stats, size_t size);
 

@@ -249,6 +249,25 @@ def test_edge_cases():
         compare(out, ref, P)
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_single_class(dtype):
+    # num_classes == 1: the blank alone, no label is ever offered (decoder.h:
+    # 146-209 loops over no label); the root is the only leaf, so only
+    # top_paths == 1 decodes.  Routed to the literal path (the fast
+    # paths' offer arithmetic divides by C - 1)
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((40, 3, 1)).astype(dtype)
+    sl = np.array([40, 0, 17], np.int32)
+    for W, blank_label in ((1, -1), (4, 0), (128, 3), (200, -1)):
+        kw = dict(merge_repeated=True, blank_index=0, blank_label=blank_label)
+        ref = oracle.decode(x, sl, W, 1, **kw)
+        out, err = _gpu_or_error(x, sl, W, 1, kw)
+        assert err is None, err
+        compare(out, ref, 1)
+    _, err = _gpu_or_error(x, sl, 4, 2, dict(merge_repeated=False, blank_index=0, blank_label=-1))
+    assert err == "Less leaves in the beam search than requested."
+
+
 def test_wide_beams():
     # R = 4 and R = 8 register tiers (beam_width > 128)
     rng = np.random.default_rng(11)
@@ -698,8 +717,19 @@ def test_one_wave_kernels_random_families(one_wave):
 DEAD = _lib.CTCEXT_FLAG_TEST_HELPER_DEAD
 
 
-@pytest.mark.parametrize("shape", [(300, 3, 29, 128, 3), (120, 2, 1000, 64, 2), (60, 2, 700, 200, 1)])
-def test_helper_timeout_strict_fails_cleanly(shape):
+# (shape, CTCEXT_HELPER): the C=29 shape under both of its two-wave kernels --
+# the default scored queue (kind 3) and the score table (kind 1), whose dead
+# path is its own (ctcx_decode.hip: `if (cx.tabdead) stop = true` before the
+# window loop, the break after its wait)
+TIMEOUT_CASES = [((300, 3, 29, 128, 3), ""), ((300, 3, 29, 128, 3), "1"),
+                 ((120, 2, 1000, 64, 2), ""), ((60, 2, 700, 200, 1), "")]
+TIMEOUT_IDS = ["c29-scored", "c29-table", "c1000", "c700-w200"]
+
+
+@pytest.mark.parametrize("shape,hmode", TIMEOUT_CASES, ids=TIMEOUT_IDS)
+def test_helper_timeout_strict_fails_cleanly(shape, hmode, monkeypatch):
+    if hmode:
+        monkeypatch.setenv("CTCEXT_HELPER", hmode)
     T, B, C, W, P = shape
     rng = np.random.default_rng(C + W)
     x = rng.standard_normal((T, B, C)).astype(np.float32)
@@ -712,16 +742,21 @@ def test_helper_timeout_strict_fails_cleanly(shape):
     # the handle stays usable: the next call decodes normally
     out = ctcext_amd.ctc_ext_beam_search_decoder(x, sl, W, P, merge_repeated=True)
     compare(out, oracle.decode(x, sl, W, P, True), P)
-    assert _stats()["helper"] in (2, 3) and _stats()["helper_redecodes"] == 0
+    assert _stats()["helper"] == (1 if hmode == "1" else 2 if W > 128 else 3), _stats()
+    assert _stats()["helper_redecodes"] == 0
 
 
-@pytest.mark.parametrize("shape", [(300, 3, 29, 128, 3), (120, 2, 1000, 64, 2), (60, 2, 700, 200, 1)])
-def test_helper_timeout_redecodes_one_wave(shape):
+@pytest.mark.parametrize("shape,hmode", TIMEOUT_CASES, ids=TIMEOUT_IDS)
+def test_helper_timeout_redecodes_one_wave(shape, hmode, monkeypatch):
+    if hmode:
+        monkeypatch.setenv("CTCEXT_HELPER", hmode)
     T, B, C, W, P = shape
     rng = np.random.default_rng(C * W)
     x = rng.standard_normal((T, B, C)).astype(np.float32)
     sl = np.full(B, T, np.int32)
-    out = ctcext_amd.ctc_ext_beam_search_decoder(x, sl, W, P, merge_repeated=True, flags=DEAD)
+    # the re-decode is never silent: the op warns
+    with pytest.warns(RuntimeWarning, match="hand-over wait timed out"):
+        out = ctcext_amd.ctc_ext_beam_search_decoder(x, sl, W, P, merge_repeated=True, flags=DEAD)
     st = _stats()
     assert st["helper_redecodes"] == 1 and st["helper"] == 0, st
     compare(out, oracle.decode(x, sl, W, P, True), P)
