@@ -278,7 +278,26 @@ struct Ctx {
   int W, C, blank, enc, hts, wcap;
   int hdum;            // he index of lane 0's dummy store slot
   int tabdead;         // HW kernels: a score-table wait gave up (never in a correct run)
+  // scored queue, small C (kCtab): branch i's children by label (cmask[i] bit
+  // l) and their positions (ctab[i * 64 + l]); null elsewhere
+  CTCX_LDS uint64_t* cmask;
+  CTCX_LDS uint8_t* ctab;
+#ifdef CTCX_PHASES
+  uint64_t* prof;      // this item's phase counters (diagnostics build; null: off)
+#endif
 };
+// the helper wave's phase counters (diagnostics build): lane 0 of wave 1 adds
+#ifdef CTCX_PHASES
+#define CTCX_HPC(cx, i, v)                                                                              \
+  do {                                                                                                  \
+    if ((cx).prof && threadIdx.x == 64)                                                                 \
+      __hip_atomic_fetch_add((cx).prof + (i), (uint64_t)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); \
+  } while (0)
+#define CTCX_HTIME() __builtin_amdgcn_s_memtime()
+#else
+#define CTCX_HPC(cx, i, v) do { } while (0)
+#define CTCX_HTIME() 0ull
+#endif
 
 // Per-64-label block maxima of the logit row, right after the row (large C).
 template <typename T>
@@ -2074,6 +2093,19 @@ __host__ __device__ constexpr int sq_slots(int wcap) { return wcap <= 128 ? kQSl
 __host__ __device__ inline size_t gq_lds_bytes(bool scored, int slots = kQSlots) {
   return (size_t)slots * ((scored ? 64 * 20 : 64 * 4) + 16);
 }
+// The scored queue at small C (C <= 64): each branch's children as a label
+// mask and a (branch, label) -> child position table, built at the commit
+// with the sibling lists, so the helper's GetChild (sq_score) is one or two
+// LDS reads instead of a walk down the branch's sibling list (one dependent
+// read pair per child: the frame's first branches, those the first chunk
+// holds, have the most children).
+#ifndef CTCX_CTAB
+#define CTCX_CTAB 1
+#endif
+constexpr bool kCtab = CTCX_CTAB != 0;
+__host__ __device__ constexpr size_t sq_ctab_bytes(int wcap, int C) {
+  return (kCtab && C <= 64) ? (size_t)wcap * 8 + (size_t)wcap * 64 : 0;
+}
 template <bool SCORED>
 __device__ __forceinline__ GQ gq_carve(CTCX_LDS char* p, int slots) {
   GQ q{};
@@ -2100,7 +2132,7 @@ __device__ __forceinline__ uint32_t sq_pack(int i, int cw, int l) {
 // branch child it re-offers (GetChild finds it; -1: none) and the child's
 // label-ending alignment candidate (decoder.h:172-185).  v: a real offer
 // (others skip the child walk).
-template <typename T>
+template <typename T, bool CT = false>   // CT: the children table (small C, kCtab)
 __device__ __forceinline__ void sq_score(const Ctx<T>& cx, int buf, T norm, bool v, int i, int l, T& s, T& bt,
                                          int& cw, Best<T>& cd) {
   const T NI = ninf<T>();
@@ -2113,7 +2145,11 @@ __device__ __forceinline__ void sq_score(const Ctx<T>& cx, int buf, T norm, bool
   const T p = cx.row[l] - norm;
   s = p + ((l == bl) ? bob : bt);
   cw = -1;
+  if constexpr (CT) {   // small C: the children table (sq_ctab_bytes)
+    if (v && ((cx.cmask[i] >> (l & 63)) & 1ull)) cw = cx.ctab[i * 64 + l];
+  } else
   for (int k = v ? hd : -1; __ballot(k >= 0);) {
+    CTCX_HPC(cx, 27, 1);
     int nk = -1;
     if (k >= 0) {
       const int lk = sel(cx.lab, buf)[k];
@@ -2146,6 +2182,7 @@ __device__ __forceinline__ void gather_small_scored(const Ctx<T>& cx, int buf, i
   const float rcp = 1.0f / (float)Cm1;
   cqn = 0;
   while (cqn < 64 && i0 < nb) {
+    CTCX_HPC(cx, 31, 1);
     const int x = li0 + lane;
     int q = (int)((float)x * rcp);
     q -= (q * Cm1 > x) ? 1 : 0;
@@ -2158,7 +2195,7 @@ __device__ __forceinline__ void gather_small_scored(const Ctx<T>& cx, int buf, i
     T s, bt;
     int cw;
     Best<T> cd;
-    sq_score<T>(cx, buf, norm, v, i, l, s, bt, cw, cd);
+    sq_score<T, kCtab>(cx, buf, norm, v, i, l, s, bt, cw, cd);
     // a turn starting in this step (label index 0) and closed at this bottom
     const uint64_t brkM = __ballot(v && li == 0 && !(bt > bottom));
     const int kb = brkM ? (int)__builtin_ctzll(brkM) : 64;
@@ -2223,9 +2260,11 @@ __device__ __forceinline__ void help_gather_scored(const Ctx<T>& cx, GQ q, int b
   const T txo = BIG ? cx.rxout : ninf<T>();
   int i0 = 0, li0 = 0, cbr = -1;
   bool gstop = false;
+  [[maybe_unused]] const uint64_t hg0 = CTCX_HTIME();
   for (int c = 0;; ++c) {
     bool done = false;
     uint64_t tw = 0;
+    [[maybe_unused]] const uint64_t hw0 = CTCX_HTIME();
     for (int spin = 0;; ++spin) {   // the grow still running, and wave 0 at most kSqLead chunks behind
       if (ctl_ld(m, kCtlDone) != 0) { done = true; break; }
       if (wait_expired(spin, tw)) {
@@ -2236,6 +2275,7 @@ __device__ __forceinline__ void help_gather_scored(const Ctx<T>& cx, GQ q, int b
       if (c < ctl_ld(m, kCtlCons) + (BIG ? 1 : kSqLead)) break;
       __builtin_amdgcn_s_sleep(CTCX_SLEEP);
     }
+    CTCX_HPC(cx, 26, CTCX_HTIME() - hw0);
     if (done) break;
     // wave 0's bottom after its last chunk (it only rises)
     const T pb = (T)__builtin_bit_cast(float, (unsigned)ctl_ld(m, kCtlBot));
@@ -2289,8 +2329,11 @@ __device__ __forceinline__ void help_gather_scored(const Ctx<T>& cx, GQ q, int b
       q.h[slot * 4 + 3] = gstop ? 1 : 0;
     }
     __hip_atomic_store(&m[kCtlReady], c + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (c == 0) CTCX_HPC(cx, 25, CTCX_HTIME() - hg0);
+    CTCX_HPC(cx, 30, 1);
     if (cqn == 0 || gstop) break;   // the last chunk of the frame
   }
+  CTCX_HPC(cx, 24, CTCX_HTIME() - hg0);
   if (BIG && cbr >= 0) cq_children(cx, buf, nb, cbr, -1);   // the child bitmap starts the next frame clear
 }
 
@@ -2479,7 +2522,11 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     if (helper_wave()) {
       if constexpr (SQ) {
         if (nb >= W) help_gather_scored<T, BIG>(cx, gq, buf, nb, norm, pmax, wave_min(lmin));
-        if constexpr (RN == 1 && kExtRank && (kExtBig || !BIG) && !kExtLate) help_rank_extract<T>(cx);
+        if constexpr (RN == 1 && kExtRank && (kExtBig || !BIG) && !kExtLate) {
+          [[maybe_unused]] const uint64_t hr0 = CTCX_HTIME();
+          help_rank_extract<T>(cx);
+          CTCX_HPC(cx, 28, CTCX_HTIME() - hr0);
+        }
       } else if constexpr (BIG) {
         // how far ahead of wave 0 the helper gathers (at most kQSlots chunks):
         // a chunk gathered early carries offers a later bottom rejects, and at
@@ -3076,7 +3123,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
         T s2, bt2;
         int c2;
         Best<T> cd2;
-        sq_score<T>(cx, buf, norm, valid, i, l, s2, bt2, c2, cd2);
+        sq_score<T, SQ && !BIG && kCtab>(cx, buf, norm, valid, i, l, s2, bt2, c2, cd2);
         const int fmask = (__builtin_bit_cast(unsigned, (float)s2) != __builtin_bit_cast(unsigned, (float)s) ? 1 : 0) |
                           (__builtin_bit_cast(unsigned, (float)bt2) != __builtin_bit_cast(unsigned, (float)bt) ? 2 : 0) |
                           (c2 != c ? 4 : 0) |
@@ -4321,6 +4368,8 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
   cx.blank = prm.blank;
   cx.sctab = prm.scorer_tab;
   cx.tabdead = 0;
+  cx.cmask = nullptr;
+  cx.ctab = nullptr;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int64_t b = blockIdx.x;
@@ -4354,6 +4403,11 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
       constexpr int kSlots = SQ ? sq_slots(WC) : kQSlots;
       gq = gq_carve<SQ>((CTCX_LDS char*)lds + off, kSlots);
       off += gq_lds_bytes(SQ, kSlots);
+      if constexpr (SQ && !BIG && kCtab) {
+        cx.cmask = (CTCX_LDS uint64_t*)((CTCX_LDS char*)lds + off);
+        cx.ctab = (CTCX_LDS uint8_t*)((CTCX_LDS char*)lds + off + (size_t)WC * 8);
+        off += sq_ctab_bytes(WC, 0);
+      }
     }
     if (R > 0) rg = ring_carve<RT>((CTCX_LDS char*)lds + off, R, W);
   }
@@ -4379,6 +4433,7 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
     cx.cb[0][0] = T(0); cx.cn[0][0] = T(0);
     cx.ha[0][0] = kRootHa; cx.hb[0][0] = kRootHb;
     cx.head[0] = -1;
+    if constexpr (SQ && !BIG && kCtab) cx.cmask[0] = 0ull;
     cx.alias[0] = 0;
     if constexpr (SC::kStateful) cx.est[0][0] = T(0);   // InitializeState (decoder.h:226)
   }
@@ -4398,6 +4453,7 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
   // per-phase s_memtime accumulators (diagnostics builds only; PhaseCtr)
   const bool prof = prm.prof != nullptr;
   const PhaseCtr pc{prof ? prm.prof + (size_t)b * kPhaseN : nullptr};
+  cx.prof = pc.p;
   if (prof && tid == 0)
     for (int q = 0; q < kPhaseN; ++q) pc.p[q] = 0;
 #else
@@ -4486,8 +4542,11 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
         cx.misc[5] = n;
         cx.misc[6] = nl_fast;
       }
-      if (helper_wave() && pf_t >= 0)   // the helper: the flush the previous commit left pending
+      if (helper_wave() && pf_t >= 0) {   // the helper: the flush the previous commit left pending
+        [[maybe_unused]] const uint64_t hf0 = CTCX_HTIME();
         ring_flush<(WC > 0 ? WC : 512) / 64, RT, true>(rg, rstream, foff, pf_t, pf_lo, pf_hi, nullptr, 0, pf_fp, nrec);
+        CTCX_HPC(cx, 29, CTCX_HTIME() - hf0);
+      }
       if constexpr (SQ && RN == 1 && kExtRank && (kExtBig || !BIG) && kExtLate)
         if (helper_wave()) help_rank_extract<T>(cx);
       pf_t = -1;
@@ -4669,12 +4728,22 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
     buf = nx;
     nb = n;
     dup = dup_next;
-    for (int k = tid; k < nb; k += NT) cx.head[k] = -1;
+    constexpr bool kCT = SQ && !BIG && kCtab;   // the scored queue's children table (sq_score)
+    for (int k = tid; k < nb; k += NT) {
+      cx.head[k] = -1;
+      if constexpr (kCT) cx.cmask[k] = 0ull;
+    }
     __syncthreads();
     for (int k = tid; k < nb; k += NT) {
       const int pp = sel(cx.par, buf)[k];
-      if (pp >= 0 && (!dup || cx.alias[k] == k))
+      if (pp >= 0 && (!dup || cx.alias[k] == k)) {
         cx.sib[k] = __hip_atomic_exchange(&cx.head[pp], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if constexpr (kCT) {   // (a parent's children have distinct labels)
+          const int lk = sel(cx.lab, buf)[k];
+          __hip_atomic_fetch_or(&cx.cmask[pp], 1ull << (lk & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          cx.ctab[pp * 64 + lk] = (uint8_t)k;
+        }
+      }
     }
     if (R == 0) nrec_all += n;
     else if (t - flushed + 1 == R) {   // the ring is full: write its older half
@@ -5859,7 +5928,9 @@ hipError_t launch_decode_c(const DecodeParams<T>& p, hipStream_t s) {
   // the decode layout, then (HW) the score table or gather queue, then the
   // record ring (its size by the same functions as the host's checks)
   size_t lds = decode_lds_bytes(WC > 0 ? WC : p.W, p.C, (int)sizeof(T), SC::kStateful);
-  if (HW) lds = ((lds + 15) & ~(size_t)15) + ((BIG || SQ) ? gq_lds_bytes(SQ, SQ ? sq_slots(WC) : kQSlots) : tab_lds_bytes());
+  if (HW)
+    lds = ((lds + 15) & ~(size_t)15) + ((BIG || SQ) ? gq_lds_bytes(SQ, SQ ? sq_slots(WC) : kQSlots) : tab_lds_bytes()) +
+          ((SQ && !BIG) ? sq_ctab_bytes(WC, 0) : 0);
   if (p.ring > 0) lds = ((lds + 15) & ~(size_t)15) + ring_lds_bytes(p.ring, p.W, HW && !BIG ? 4 : 8);
   if (lds > kLdsBytes) return hipErrorInvalidValue;
   if (lds > 64 * 1024) {
@@ -6027,7 +6098,10 @@ __host__ inline int helper_wc(int W) { return W <= 128 ? 128 : 256; }
 template <typename T>
 size_t pre_ring_lds_bytes(const DecodeParams<T>& p, int hk, int wc) {
   const size_t b = (decode_lds_bytes(wc, p.C, (int)sizeof(T), p.scorer_tab != nullptr) + 15) & ~(size_t)15;
-  return hk == 1 ? b + tab_lds_bytes() : hk == 2 ? b + gq_lds_bytes(false) : hk == 3 ? b + gq_lds_bytes(true, sq_slots(wc)) : b;
+  return hk == 1   ? b + tab_lds_bytes()
+         : hk == 2 ? b + gq_lds_bytes(false)
+         : hk == 3 ? b + gq_lds_bytes(true, sq_slots(wc)) + (p.C <= 64 ? sq_ctab_bytes(wc, (int)p.C) : 0)
+                   : b;
 }
 // the two-wave kernel this call runs (0: none), given the kind the host chose
 // (hk): its layout and ring must fit

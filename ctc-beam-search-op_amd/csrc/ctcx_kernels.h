@@ -19,7 +19,7 @@ namespace ctcx {
 // 3 extract, 4 commit, 5 literal frames, 6 grow events, 7 frames, 8 offer
 // scoring, 9 event loops, 10 heap pushes, 11 offer chunks, 12 accepted
 // events, 13 heap pushes (count)
-constexpr int kPhaseN = 24;
+constexpr int kPhaseN = 32;   // [0, 24): wave 0, [24, 32): the helper wave (CTCX_PHASES)
 
 constexpr uint32_t kBpRestart = 0xFFFFFFFEu;  // candidate started a new chain
 constexpr uint32_t kBpNone = 0xFFFFFFFFu;     // no candidate of that kind

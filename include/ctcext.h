@@ -196,10 +196,12 @@ int ctcext_get_stats_sized(ctcext_decoder* dec, ctcext_stats* stats, size_t size
 /* CTCEXT_ABI_VERSION of the library. */
 int32_t ctcext_abi_version(void);
 
-/* Diagnostics: copies the [batch][16] phase counters of the last decode run
- * with CTCEXT_FLAG_PHASES (cycles: row load, recursion, grow, extract, commit,
- * literal frames; counts: grow events, frames; cycles: offer scoring, event
- * loops, heap pushes; counts: offer chunks, accepted events, heap pushes). */
+/* Diagnostics: copies the [batch][32] phase counters of the last decode run
+ * with CTCEXT_FLAG_PHASES, in the diagnostics build (make phases; the product
+ * build leaves them 0).  [0, 24) the decoding wave (cycles: row load,
+ * recursion, grow, extract, commit, literal frames; counts: grow events,
+ * frames; ... see tools/diag_phases.py for every index), [24, 32) the helper
+ * wave of the two-wave kernels. */
 int ctcext_phase_counters(ctcext_decoder* dec, uint64_t* out, int64_t n);
 
 /* Diagnostics (tests): the pre-pass of a decode alone, on device buffers and

@@ -17,8 +17,11 @@ f = _lib.CTCEXT_FLAG_PHASES | _lib.CTCEXT_FLAG_PROFILE
 ctcext_amd.ctc_ext_beam_search_decoder(x, sl, W, P, merge_repeated=True, flags=f)
 out = ctcext_amd.ctc_ext_beam_search_decoder(x, sl, W, P, merge_repeated=True, flags=f)
 d = ctcext_amd.get_decoder(0)
-buf = np.zeros((B, 24), np.uint64)
-d.lib.ctcext_phase_counters(d.handle, ctypes.c_void_p(buf.ctypes.data), B * 24)
+NPH = 32   # ctcx_kernels.h kPhaseN: [0, 24) wave 0, [24, 32) the helper wave
+buf = np.zeros((B, NPH), np.uint64)
+rc = d.lib.ctcext_phase_counters(d.handle, ctypes.c_void_p(buf.ctypes.data), B * NPH)
+if rc != 0:
+    sys.exit("ctcext_phase_counters failed (%d): %s" % (rc, d.lib.ctcext_last_error().decode()))
 m = buf.astype(np.float64).mean(0)
 fr = m[7]
 names = ["rowload", "recursion", "grow", "extract", "commit", "literal", "heap events", "frames",
@@ -54,3 +57,10 @@ if True:
     print("  HW waves: same CU %d/%d items, same SIMD %d/%d items (wave0 SIMD histogram %s, helper %s)" % (
         int(same_cu.sum()), B, int((same_cu & (simd0 == simd1)).sum()), B,
         np.bincount(simd0, minlength=4).tolist(), np.bincount(simd1, minlength=4).tolist()))
+# the helper wave (two-wave scored-queue kernels; 0 where it does not run)
+hn = {24: "helper gather (whole)", 25: "helper to first chunk", 26: "helper waits for wave 0",
+      28: "helper rank extract", 29: "helper ring flush"}
+for k, name in hn.items():
+    print("  %-26s %10.0f cycles/frame" % (name, m[k] / fr))
+print("  helper chunks %.2f/frame, scan steps %.2f/frame, child-walk steps %.2f/frame"
+      % (m[30] / fr, m[31] / fr, m[27] / fr))

@@ -9,3 +9,7 @@ timeout -k 10 400 python bench.py > $O/bench_cfg3.json 2> $O/bench_cfg3.err || e
 echo "[$(date +%T)] ab" >> $O/steps.log
 for cfg in cfg3 cfg4; do echo "== $cfg" >> $O/summary.txt; CFG=$cfg bash tools/abv.sh 2 'r5||abrun/libr5.so|' 'r6||' >> $O/summary.txt 2>&1 || exit 13; done
 echo "[$(date +%T)] done" >> $O/steps.log
+echo "[$(date +%T)] phases" >> $O/steps.log
+PHASES_LIB=$R/abrun/libctcext_phases.so bash tools/gpu_phases.sh || exit 14
+for c in cfg3 cfg4 cfg5; do mv gpurun_out/ph_$c.txt $O/ph_$c.txt; done
+echo "[$(date +%T)] done2" >> $O/steps.log

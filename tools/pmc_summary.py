@@ -39,6 +39,31 @@ def per_launch(path, counter, kname):
     return sum(vals) / len(vals), len(vals), name
 
 
+def all_kernels(fetch_path, write_path, f_read, f_write):
+    """Every kernel of the decode call in the two passes (the pre-pass, the
+    decode, the traceback and packing): per-launch corrected bytes and their
+    sum over one call (each kernel runs once per call)."""
+    acc = {}
+    for path, counter in ((fetch_path, "FETCH_SIZE"), (write_path, "WRITE_SIZE")):
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                if row["Counter_Name"] != counter:
+                    continue
+                k = row["Kernel_Name"]
+                if "ctcx" not in k:   # (torch's own kernels: input generation, copies)
+                    continue
+                e = acc.setdefault(k, {"FETCH_SIZE": [], "WRITE_SIZE": []})
+                e[counter].append(float(row["Counter_Value"]))
+    out, call = {}, 0.0
+    for k, e in sorted(acc.items()):
+        rd = (sum(e["FETCH_SIZE"]) / len(e["FETCH_SIZE"]) * 1024 * f_read) if e["FETCH_SIZE"] else 0.0
+        wr = (sum(e["WRITE_SIZE"]) / len(e["WRITE_SIZE"]) * 1024 * f_write) if e["WRITE_SIZE"] else 0.0
+        out[k.split("(")[0]] = {"read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
+                               "launches": [len(e["FETCH_SIZE"]), len(e["WRITE_SIZE"])]}
+        call += rd + wr
+    return out, call
+
+
 def main():
     fetch_csv, write_csv, cfg, seq_len, cf_csv, cw_csv, calib_json = sys.argv[1:8]
     known = json.load(open(calib_json))
@@ -74,6 +99,11 @@ def main():
                   "each counter scaled by the factor tools/fetch_calib.hip measured for the same access "
                   "pattern over a known byte count in the same pass" % cfg,
     }
+    # the whole call: every kernel's bytes (reads at the stream16 factor for
+    # the large-C pre-pass and rows, writes at the record factor)
+    ak, call = all_kernels(fetch_csv, write_csv, f_s16 if pattern == "stream16" else f_rows, f_rec)
+    out["all_kernels"] = ak
+    out["hbm_bytes_per_call"] = call
     print(json.dumps(out, indent=1))
 
 
