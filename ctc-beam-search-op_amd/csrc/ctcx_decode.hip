@@ -278,10 +278,6 @@ struct Ctx {
   int W, C, blank, enc, hts, wcap;
   int hdum;            // he index of lane 0's dummy store slot
   int tabdead;         // HW kernels: a score-table wait gave up (never in a correct run)
-  // scored queue, small C (kCtab): branch i's children by label (cmask[i] bit
-  // l) and their positions (ctab[i * 64 + l]); null elsewhere
-  CTCX_LDS uint64_t* cmask;
-  CTCX_LDS uint8_t* ctab;
 #ifdef CTCX_PHASES
   uint64_t* prof;      // this item's phase counters (diagnostics build; null: off)
 #endif
@@ -875,6 +871,9 @@ __device__ __forceinline__ void wave_push_heap_v(CTCX_LDS HE<T>* he, const HeapG
 __device__ __forceinline__ int writelane(int old, int val, int lane) {
   return __builtin_amdgcn_inverse_ballot_w64(1ull << lane) ? val : old;
 }
+__device__ __forceinline__ float writelane(float old, float val, int lane) {
+  return __builtin_amdgcn_inverse_ballot_w64(1ull << lane) ? val : old;
+}
 
 __device__ __forceinline__ uint64_t lowmask(int n) { return n >= 64 ? ~0ull : ((1ull << n) - 1ull); }
 
@@ -1035,6 +1034,25 @@ __device__ __forceinline__ void mpush(CTCX_LDS HE<T>* he, const typename MaskGeo
 // later (or behind an s_nop); DS operand registers are rewritten only after
 // the s_waitcnt lgkmcnt(0) that retires their instruction; lane selects come
 // from SALU.  Temporaries: s84..s99, vcc, v232..v243 (clobbered).
+// The bottom each lane's branch turn sees (bat; decoder.h:151-159): read
+// only for one lane at a time (a re-offer's lane, the chunk's last lane), so
+// with CTCX_BAT_LAZY the loop records the front after each push in lane k of
+// fa (one v_writelane, m0 = k) instead of refreshing bat in every later turn's
+// lane (a compare, a move and a select per push); the caller derives a lane's
+// bat from the last push before its turn start (bat_of in exact_step).
+#ifndef CTCX_BAT_LAZY
+#define CTCX_BAT_LAZY 0
+#endif
+#if CTCX_BAT_LAZY
+#define CTCX_BAT_A ""
+#define CTCX_BAT_B "v_writelane_b32 %[bat], %[fv], m0\n\t"   /* fa[k] = the front after push k */
+#define CTCX_BAT_C ""
+#else
+#define CTCX_BAT_A "v_cmp_lt_i32_e64 vcc, %[k], %[sl]\n\t"   /* turns starting after lane k see the new bottom */
+#define CTCX_BAT_B "v_mov_b32_e32 v242, %[fv]\n\t"
+#define CTCX_BAT_C "v_cndmask_b32_e32 %[bat], %[bat], v242, vcc\n\t"
+#endif
+constexpr bool kBatLazy = CTCX_BAT_LAZY != 0;
 #ifdef CTCX_PHASES
 #define CTCX_EVCNT "s_add_u32 %[cnt], %[cnt], 1\n\t"   // diagnostics builds: count the pushes
 #else
@@ -1094,11 +1112,11 @@ __device__ __forceinline__ int heap_events_f32(float s, int c, int sl, unsigned 
       "s_cselect_b32 %[fv], s84, s86\n\t"                  // the new front
       "s_cselect_b32 %[fs], s85, s87\n\t"
       "s_or_b32 s98, s98, s96\n\t"                         // cnd: gt, or the min child is a non-lane leaf
-      "v_cmp_lt_i32_e64 vcc, %[k], %[sl]\n\t"              // turns starting after lane k see the new bottom
+      CTCX_BAT_A
       "v_cmp_lt_f32_e64 s[88:89], %[fv], %[s]\n\t"         // next: s > front
       "s_and_b64 s[90:91], s[94:95], s[98:99]\n\t"         // cm (path nodes meeting the stop condition)
       "s_ff1_i32_b64 s86, s[90:91]\n\t"                    // the stop: the shallowest of them
-      "v_mov_b32_e32 v242, %[fv]\n\t"
+      CTCX_BAT_B
       "s_lshl_b64 s[90:91], -2, s86\n\t"
       "s_andn2_b64 s[94:95], s[94:95], s[90:91]\n\t"       // live: path nodes at or above the stop
       "s_andn2_b64 s[90:91], s[94:95], s[96:97]\n\t"       // up: takes its min child
@@ -1108,7 +1126,7 @@ __device__ __forceinline__ int heap_events_f32(float s, int c, int sl, unsigned 
       "ds_write2_b32 v239, v237, v238 offset1:1\n\t"
       "ds_write2_b32 v236, v240, v241 offset1:1\n\t"
       "ds_read_b128 v[232:235], %[al]\n\t"                 // the next push's child pairs
-      "v_cndmask_b32_e32 %[bat], %[bat], v242, vcc\n\t"
+      CTCX_BAT_C
       "s_and_b64 s[88:89], s[88:89], %[nc]\n\t"
       "s_or_b64 s[88:89], s[88:89], %[rb]\n\t"
       "s_and_b64 s[88:89], s[88:89], s[80:81]\n\t"         // next m
@@ -1216,14 +1234,14 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
       "s_bitcmp1_b32 s96, 0\n\t"                           // keep: v stays at the root
       "s_cselect_b32 %[fv], s84, s86\n\t"                  // the new front
       "s_cselect_b32 %[fs], s85, s87\n\t"
-      "v_cmp_lt_i32_e64 vcc, %[k], %[sl]\n\t"              // turns starting after lane k see the new bottom
+      CTCX_BAT_A
       "v_cmp_lt_f32_e64 s[88:89], %[fv], %[s]\n\t"         // next: s > front
       "v_cndmask_b32_e64 v253, v253, %[aj1], %[g1]\n\t"
       "s_and_b64 s[90:91], s[94:95], s[98:99]\n\t"         // cm0
       "s_cmp_eq_u64 s[90:91], 0\n\t"
       "s_cselect_b64 %[o1], %[o1], 0\n\t"                  // live1: the path's group-1 node, when group 0 has no stop
       "s_ff1_i32_b64 s86, s[90:91]\n\t"                    // the stop (-1: in group 1)
-      "v_mov_b32_e32 v242, %[fv]\n\t"
+      CTCX_BAT_B
       "s_lshl_b64 s[90:91], -2, s86\n\t"
       "s_andn2_b64 s[94:95], s[94:95], s[90:91]\n\t"       // live0
       "s_andn2_b64 s[90:91], s[94:95], s[96:97]\n\t"       // up0
@@ -1239,7 +1257,7 @@ __device__ __forceinline__ int heap_events_m2_f32(float s, int c, int sl, unsign
       "ds_write2_b32 v253, v240, v241 offset1:1\n\t"
       "ds_read_b128 v[232:235], %[al]\n\t"                 // the next push's child pairs
       "ds_read_b128 v[244:247], %[al] offset:1024\n\t"
-      "v_cndmask_b32_e32 %[bat], %[bat], v242, vcc\n\t"
+      CTCX_BAT_C
       "s_and_b64 s[88:89], s[88:89], %[nc]\n\t"
       "s_or_b64 s[88:89], s[88:89], %[rb]\n\t"
       "s_and_b64 s[88:89], s[88:89], s[80:81]\n\t"         // next m
@@ -2084,6 +2102,11 @@ struct GQ {
   CTCX_LDS u32x4* a;        // [slot][64]: scored offers (SQ)
   CTCX_LDS float* p;        // [slot][64]: their candidate values (SQ)
   int sm;                   // slots - 1 (a power of two)
+  // SQ, small C (kCtab, sq_ctab_bytes): branch i's children by label (cmask[i]
+  // bit l) and their positions (ctab[i * 64 + l]).  (Here, not in Ctx: Ctx
+  // goes by value to the literal step's call, whose register use then moves.)
+  CTCX_LDS uint64_t* cmask;
+  CTCX_LDS uint8_t* ctab;
 };
 // Scored slots per kernel: four for beams <= 128; one for beams of 129..256,
 // whose layout must stay under half a CU (cfg5: 80.1 KB of the 80 KB, a
@@ -2105,6 +2128,37 @@ __host__ __device__ inline size_t gq_lds_bytes(bool scored, int slots = kQSlots)
 constexpr bool kCtab = CTCX_CTAB != 0;
 __host__ __device__ constexpr size_t sq_ctab_bytes(int wcap, int C) {
   return (kCtab && C <= 64) ? (size_t)wcap * 8 + (size_t)wcap * 64 : 0;
+}
+// Large C, beams of up to 256 (BIG kernels, WC > 0): GetChild through a
+// (parent, label) -> child hash table instead of a walk down the parent's
+// sibling list (up to one dependent LDS read pair per child of the branch:
+// at C = 5000, W = 256 the best branches hold tens of the beam's entries).
+// It lives in the per-frame new-leaf hash table's room (htab, >= 2W words),
+// which the commit no longer needs once its parents are linked: the commit
+// rebuilds it with the sibling lists, one word per branch
+// (parent << 24 | label << 8 | position; -1 empty), linear probing.  The
+// literal path's free list shares that room and runs instead of a grow; the
+// next commit rebuilds the table.
+#ifndef CTCX_CHASH
+#define CTCX_CHASH 1
+#endif
+constexpr bool kCHash = CTCX_CHASH != 0;
+__device__ __forceinline__ int chash_slot(uint32_t key, int hts) { return (int)(((key * 0x9E3779B1u) >> 12) & (uint32_t)(hts - 1)); }
+template <typename T>
+__device__ __forceinline__ int chash_find(const Ctx<T>& cx, bool v, int i, int l) {
+  const uint32_t key = ((uint32_t)i << 16) | (uint32_t)l;   // (parent, label)
+  int q = v ? chash_slot(key, cx.hts) : 0;
+  int cw = -1;
+  bool go = v;
+  while (__ballot(go)) {
+    if (go) {
+      const uint32_t w = (uint32_t)cx.htab[q];
+      if (w == 0xFFFFFFFFu) go = false;
+      else if ((w >> 8) == key) { cw = (int)(w & 255u); go = false; }
+      else q = (q + 1) & (cx.hts - 1);
+    }
+  }
+  return cw;
 }
 template <bool SCORED>
 __device__ __forceinline__ GQ gq_carve(CTCX_LDS char* p, int slots) {
@@ -2132,9 +2186,10 @@ __device__ __forceinline__ uint32_t sq_pack(int i, int cw, int l) {
 // branch child it re-offers (GetChild finds it; -1: none) and the child's
 // label-ending alignment candidate (decoder.h:172-185).  v: a real offer
 // (others skip the child walk).
-template <typename T, bool CT = false>   // CT: the children table (small C, kCtab)
+template <typename T, bool CT = false, bool CH = false>   // CT: the children table (small C), CH: the child hash
 __device__ __forceinline__ void sq_score(const Ctx<T>& cx, int buf, T norm, bool v, int i, int l, T& s, T& bt,
-                                         int& cw, Best<T>& cd) {
+                                         int& cw, Best<T>& cd, const CTCX_LDS uint64_t* cmask = nullptr,
+                                         const CTCX_LDS uint8_t* ctab = nullptr) {
   const T NI = ninf<T>();
   const int bl = sel(cx.lab, buf)[i];
   const int bflg = sel(cx.flg, buf)[i];
@@ -2146,7 +2201,9 @@ __device__ __forceinline__ void sq_score(const Ctx<T>& cx, int buf, T norm, bool
   s = p + ((l == bl) ? bob : bt);
   cw = -1;
   if constexpr (CT) {   // small C: the children table (sq_ctab_bytes)
-    if (v && ((cx.cmask[i] >> (l & 63)) & 1ull)) cw = cx.ctab[i * 64 + l];
+    if (v && ((cmask[i] >> (l & 63)) & 1ull)) cw = ctab[i * 64 + l];
+  } else if constexpr (CH) {   // large C: the child hash (kCHash)
+    cw = chash_find(cx, v, i, l);
   } else
   for (int k = v ? hd : -1; __ballot(k >= 0);) {
     CTCX_HPC(cx, 27, 1);
@@ -2176,7 +2233,7 @@ __device__ __forceinline__ void sq_score(const Ctx<T>& cx, int buf, T norm, bool
 template <typename T>
 __device__ __forceinline__ void gather_small_scored(const Ctx<T>& cx, int buf, int nb, T norm, T bottom, int& i0,
                                                     int& li0, bool& gstop, CTCX_LDS u32x4* qa, CTCX_LDS float* qp,
-                                                    int& cqn, bool one_step) {
+                                                    int& cqn, bool one_step, const GQ& gq) {
   const int lane = threadIdx.x & 63;
   const int Cm1 = cx.C - 1, blank = cx.blank;
   const float rcp = 1.0f / (float)Cm1;
@@ -2195,7 +2252,7 @@ __device__ __forceinline__ void gather_small_scored(const Ctx<T>& cx, int buf, i
     T s, bt;
     int cw;
     Best<T> cd;
-    sq_score<T, kCtab>(cx, buf, norm, v, i, l, s, bt, cw, cd);
+    sq_score<T, kCtab>(cx, buf, norm, v, i, l, s, bt, cw, cd, gq.cmask, gq.ctab);
     // a turn starting in this step (label index 0) and closed at this bottom
     const uint64_t brkM = __ballot(v && li == 0 && !(bt > bottom));
     const int kb = brkM ? (int)__builtin_ctzll(brkM) : 64;
@@ -2305,7 +2362,7 @@ __device__ __forceinline__ void help_gather_scored(const Ctx<T>& cx, GQ q, int b
       T s, bt;
       int cw;
       Best<T> cd;
-      sq_score<T>(cx, buf, norm, v, i, l, s, bt, cw, cd);
+      sq_score<T, false, kCHash>(cx, buf, norm, v, i, l, s, bt, cw, cd);
       wsync<true>();
       if (v) {
         u32x4 ev;
@@ -2320,7 +2377,7 @@ __device__ __forceinline__ void help_gather_scored(const Ctx<T>& cx, GQ q, int b
       // the frame's first chunk: the first scan step's offers only, so wave 0
       // starts after one step instead of a full chunk (the helper gathers the
       // next chunk meanwhile)
-      gather_small_scored<T>(cx, buf, nb, norm, bottom, i0, li0, gstop, qa, qp, cqn, kSqFirst1 && c == 0);
+      gather_small_scored<T>(cx, buf, nb, norm, bottom, i0, li0, gstop, qa, qp, cqn, kSqFirst1 && c == 0, q);
     }
     if (lane == 0) {
       q.h[slot * 4 + 0] = cqn;
@@ -3123,7 +3180,8 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
         T s2, bt2;
         int c2;
         Best<T> cd2;
-        sq_score<T, SQ && !BIG && kCtab>(cx, buf, norm, valid, i, l, s2, bt2, c2, cd2);
+        sq_score<T, SQ && !BIG && kCtab, BIG && kCHash && RN <= 2>(cx, buf, norm, valid, i, l, s2, bt2, c2, cd2,
+                                                                   gq.cmask, gq.ctab);
         const int fmask = (__builtin_bit_cast(unsigned, (float)s2) != __builtin_bit_cast(unsigned, (float)s) ? 1 : 0) |
                           (__builtin_bit_cast(unsigned, (float)bt2) != __builtin_bit_cast(unsigned, (float)bt) ? 2 : 0) |
                           (c2 != c ? 4 : 0) |
@@ -3223,6 +3281,9 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       // the branch child this offer re-offers, if any (GetChild finds it): walk
       // branch i's children, each step one read pair (label, next sibling)
       c = -1;
+      if constexpr (BIG && kCHash && RN <= 2) {   // large C: the child hash (kCHash)
+        c = chash_find(cx, live, i, l);
+      } else
       for (int k = live ? hd : -1; __ballot(k >= 0);) {
         int nk = -1;
         if (k >= 0) {
@@ -3287,30 +3348,47 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
           const unsigned heb = (unsigned)(uintptr_t)he;   // LDS byte address of he[0]
           const unsigned aj = heb + 8u * (unsigned)(lane + 1), al = heb + 8u * (unsigned)(2 * lane + 2);
           const unsigned ar = al + 8u, dum = heb + 8u * (unsigned)(cx.hdum + lane);
+          // kBatLazy: the front after each push of this path in lane k of fa
+          // (NaN: no push); lane j's bat is then fa at the last push before its
+          // turn start, else bat as this path found it (bat_of)
+          float fa = __builtin_nanf("");
+          auto bat_of = [&](int j) -> float {   // (j uniform)
+            const int sj = bcast(sl, j);
+            const uint64_t pm = sj > 0 ? __ballot(fa == fa) & lowmask(sj) : 0ull;
+            return pm ? bcast(fa, 63 - __builtin_clzll(pm)) : bcast((float)bat, j);
+          };
           for (;;) {
             int k;
             fv = uni(fv); fs = uni(fs); nfree = uni(nfree); nv = uni(nv);
             int nev_asm = 0;
             const uint64_t ta = pc ? __builtin_amdgcn_s_memtime() : 0;
             int est;
+            float& bref = kBatLazy ? fa : bat;
             if constexpr (RN == 1) {
-              est = heap_events_f32(s, c, sl, geo.anc, geo.req, aj, al, ar, dum, myslot, evr, bat, NC, RB, done, LB,
+              est = heap_events_f32(s, c, sl, geo.anc, geo.req, aj, al, ar, dum, myslot, evr, bref, NC, RB, done, LB,
                                     fv, fs, nfree, nv, uni(nb), k, nev_asm);
             } else {
               est = heap_events_m2_f32(s, c, sl, geo.g.anc, geo.g.req, (unsigned)geo.anc1, (unsigned)(geo.anc1 >> 32),
                                        (unsigned)geo.req1, (unsigned)(geo.req1 >> 32), aj, al, ar, aj + 512u,
-                                       al + 1024u, ar + 1024u, dum, myslot, evr, bat, NC, RB, done, LB, fv, fs,
+                                       al + 1024u, ar + 1024u, dum, myslot, evr, bref, NC, RB, done, LB, fv, fs,
                                        nfree, nv, nb, k, nev_asm);
             }
             if (pc) { pc[13] += __builtin_amdgcn_s_memtime() - ta; pc[6] += uni(nev_asm); pc[12] += 1; }
-            if (est == 0) break;
+            if (est == 0) {
+              if constexpr (kBatLazy) {   // the chunk-end turn check reads one lane's bat
+                const int j = (BIG || SQ) ? cqn - 1 : 63;
+                const float bj = bat_of(j);
+                bat = (lane == j) ? bj : bat;
+              }
+              break;
+            }
             k = uni(k);
             // lane k re-offers a branch child.  Only a re-offer can make a closed
             // turn visible (a closed branch's new children score <= its total <=
             // bottom): was k's turn skipped?
             const uint64_t gtM = __ballot(s > fv);
             const uint64_t m = ((gtM & NC) | RB) & ~done;   // its lowest lane is k
-            if ((__ballot(!(bt > bat)) >> k) & 1ull) {
+            if (kBatLazy ? !(bcast(bt, k) > bat_of(k)) : ((__ballot(!(bt > bat)) >> k) & 1ull)) {
               const uint64_t keepM = lowmask(bcast(sl, k));   // that branch and every later one
               NC &= keepM; LB &= keepM; RB &= keepM;
               stop = true;
@@ -3344,7 +3422,8 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
             mpush<T, RN>(he, geo, k_s, kc, pp, c0, s0, keep);
             fv = keep ? k_s : c0;
             fs = keep ? kc : s0;
-            bat = (sl > k) ? fv : bat;
+            if constexpr (kBatLazy) fa = writelane(fa, uni(fv), k);
+            else bat = (sl > k) ? fv : bat;
           }
         } else {
           for (;;) {
@@ -4368,8 +4447,6 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
   cx.blank = prm.blank;
   cx.sctab = prm.scorer_tab;
   cx.tabdead = 0;
-  cx.cmask = nullptr;
-  cx.ctab = nullptr;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int64_t b = blockIdx.x;
@@ -4404,8 +4481,8 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
       gq = gq_carve<SQ>((CTCX_LDS char*)lds + off, kSlots);
       off += gq_lds_bytes(SQ, kSlots);
       if constexpr (SQ && !BIG && kCtab) {
-        cx.cmask = (CTCX_LDS uint64_t*)((CTCX_LDS char*)lds + off);
-        cx.ctab = (CTCX_LDS uint8_t*)((CTCX_LDS char*)lds + off + (size_t)WC * 8);
+        gq.cmask = (CTCX_LDS uint64_t*)((CTCX_LDS char*)lds + off);
+        gq.ctab = (CTCX_LDS uint8_t*)((CTCX_LDS char*)lds + off + (size_t)WC * 8);
         off += sq_ctab_bytes(WC, 0);
       }
     }
@@ -4433,7 +4510,7 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
     cx.cb[0][0] = T(0); cx.cn[0][0] = T(0);
     cx.ha[0][0] = kRootHa; cx.hb[0][0] = kRootHb;
     cx.head[0] = -1;
-    if constexpr (SQ && !BIG && kCtab) cx.cmask[0] = 0ull;
+    if constexpr (SQ && !BIG && kCtab) gq.cmask[0] = 0ull;
     cx.alias[0] = 0;
     if constexpr (SC::kStateful) cx.est[0][0] = T(0);   // InitializeState (decoder.h:226)
   }
@@ -4731,7 +4808,7 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
     constexpr bool kCT = SQ && !BIG && kCtab;   // the scored queue's children table (sq_score)
     for (int k = tid; k < nb; k += NT) {
       cx.head[k] = -1;
-      if constexpr (kCT) cx.cmask[k] = 0ull;
+      if constexpr (kCT) gq.cmask[k] = 0ull;
     }
     __syncthreads();
     for (int k = tid; k < nb; k += NT) {
@@ -4740,8 +4817,8 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
         cx.sib[k] = __hip_atomic_exchange(&cx.head[pp], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if constexpr (kCT) {   // (a parent's children have distinct labels)
           const int lk = sel(cx.lab, buf)[k];
-          __hip_atomic_fetch_or(&cx.cmask[pp], 1ull << (lk & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          cx.ctab[pp * 64 + lk] = (uint8_t)k;
+          __hip_atomic_fetch_or(&gq.cmask[pp], 1ull << (lk & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          gq.ctab[pp * 64 + lk] = (uint8_t)k;
         }
       }
     }
