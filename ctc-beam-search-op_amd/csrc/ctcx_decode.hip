@@ -4514,6 +4514,10 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
     cx.alias[0] = 0;
     if constexpr (SC::kStateful) cx.est[0][0] = T(0);   // InitializeState (decoder.h:226)
   }
+#ifndef CTCX_GSTATE
+  if constexpr (BIG && kCHash && RN <= 2)   // the child hash starts empty (the root has no children)
+    for (int q = tid; q < cx.hts; q += NT) cx.htab[q] = -1;
+#endif
   if constexpr (BIG) {   // the child bitmap and window summary start (and stay, between branches) clear
     const int nw = (C - 1 + 63) / 64;
     CTCX_LDS uint64_t* z = row_cbm(cx);
@@ -4806,10 +4810,13 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
     nb = n;
     dup = dup_next;
     constexpr bool kCT = SQ && !BIG && kCtab;   // the scored queue's children table (sq_score)
+    constexpr bool kCH = BIG && kCHash && RN <= 2;   // the child hash (chash_find), in htab's room
     for (int k = tid; k < nb; k += NT) {
       cx.head[k] = -1;
       if constexpr (kCT) gq.cmask[k] = 0ull;
     }
+    if constexpr (kCH)   // (the commit's parent links are done: its prefix-hash entries are dead)
+      for (int q = tid; q < cx.hts; q += NT) cx.htab[q] = -1;
     __syncthreads();
     for (int k = tid; k < nb; k += NT) {
       const int pp = sel(cx.par, buf)[k];
@@ -4819,6 +4826,17 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
           const int lk = sel(cx.lab, buf)[k];
           __hip_atomic_fetch_or(&gq.cmask[pp], 1ull << (lk & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           gq.ctab[pp * 64 + lk] = (uint8_t)k;
+        }
+        if constexpr (kCH) {   // (parent, label) -> k: parent < 256, label < 65535, k < 256
+          const uint32_t key = ((uint32_t)pp << 16) | (uint32_t)sel(cx.lab, buf)[k];
+          const int w = (int)((key << 8) | (uint32_t)k);
+          int q = chash_slot(key, cx.hts);
+          int expect = -1;
+          while (!__hip_atomic_compare_exchange_strong(&cx.htab[q], &expect, w, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            q = (q + 1) & (cx.hts - 1);
+            expect = -1;
+          }
         }
       }
     }

@@ -150,3 +150,20 @@ def test_oracle_scorer_hook():
     for f in lm._fields:
         for a, b in zip(getattr(lm, f), getattr(lmf, f)):
             np.testing.assert_array_equal(a, b)
+
+
+def test_bench_digest_fixture_reproduces():
+    # tests/golden/bench_digests.json pins bench.py's outputs_match_oracle: the
+    # oracle's outputs for the exact bench inputs, hashed by bench.output_digest.
+    # Rank 0 of cfg2 (B=32, T=1000) recomputed here, in item shards as the
+    # generator runs them (the items are independent, kernels.cc:68-90)
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    B, T, C, W, P, merge, blank = bench.CONFIGS["cfg2"]
+    fx = json.load(open(os.path.join(root, "tests", "golden", "bench_digests.json")))["cfg2"]
+    assert (fx["batch_per_gpu"], fx["seq_len"], fx["num_classes"], fx["beam_width"]) == (B, T, C, W)
+    x = np.random.default_rng(20251015).standard_normal((T, B, C), dtype=np.float32)
+    out = oracle.decode(x, np.full(B, T, np.int32), W, P, merge, blank, -1)
+    assert bench.output_digest(out, P) == fx["digests"]["0"]
