@@ -2123,7 +2123,7 @@ __host__ __device__ inline size_t gq_lds_bytes(bool scored, int slots = kQSlots)
 // read pair per child: the frame's first branches, those the first chunk
 // holds, have the most children).
 #ifndef CTCX_CTAB
-#define CTCX_CTAB 1
+#define CTCX_CTAB 0
 #endif
 constexpr bool kCtab = CTCX_CTAB != 0;
 __host__ __device__ constexpr size_t sq_ctab_bytes(int wcap, int C) {
@@ -2140,7 +2140,7 @@ __host__ __device__ constexpr size_t sq_ctab_bytes(int wcap, int C) {
 // literal path's free list shares that room and runs instead of a grow; the
 // next commit rebuilds the table.
 #ifndef CTCX_CHASH
-#define CTCX_CHASH 1
+#define CTCX_CHASH 0
 #endif
 constexpr bool kCHash = CTCX_CHASH != 0;
 __device__ __forceinline__ int chash_slot(uint32_t key, int hts) { return (int)(((key * 0x9E3779B1u) >> 12) & (uint32_t)(hts - 1)); }
