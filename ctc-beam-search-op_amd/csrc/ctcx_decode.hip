@@ -5959,6 +5959,167 @@ __global__ __launch_bounds__(256) void ctcx_traceback(TraceParams tp) {
   tp.len[((int64_t)p * 2 + which) * tp.len_stride + b] = len;
 }
 
+// The same walks, one 256-thread block per item (2P <= 256 walkers), through
+// LDS copies of the item's records: every walker of an item is at the same
+// frame at every step (each step goes one frame back), so the records of G
+// frames at a time -- one contiguous range of the item's stream, the ring's
+// compacted frames or [t][W] -- are copied in with 16-byte loads and the
+// walkers step through LDS, where ctcx_traceback waits out one dependent
+// global load per frame (~1.1 us at cfg3: 1.74 ms for 1500 frames).  Two
+// buffers: the next segment's loads are in flight, in registers, while the
+// walkers step through the current one.
+// (static LDS stays within the 64 KB a plain launch gets: two 24-KB buffers
+// and the offsets, 56 KB -- at 72 KB the launch ran with 64 and the offsets
+// past it read as 0)
+constexpr int kTbBufBytes = 24 * 1024;           // one segment buffer
+constexpr int kTbLoads = kTbBufBytes / 16 / 256;  // 16-byte loads per thread per segment
+static_assert(kTbLoads * 16 * 256 == kTbBufBytes, "whole loads");
+constexpr int kTbMaxG = 1024;                     // frames per segment at most (the offsets' buffer)
+__device__ __forceinline__ void tb_rec(const uint32_t* w, int rb, uint32_t& link, int& lab, uint32_t& bpb,
+                                       uint32_t& bpn) {   // one record from its first word in LDS
+  if (rb == 16) {
+    const uint4 r = *(const uint4*)w;
+    link = r.x; lab = (int)r.y; bpb = r.z; bpn = r.w;
+  } else if (rb == 4) {
+    const uint32_t r = w[0];
+    link = r & 255u; lab = (int)((r >> 8) & 63u); bpb = rec32_unbp9((r >> 14) & 511u); bpn = rec32_unbp9(r >> 23);
+  } else {
+    const uint2 u = *(const uint2*)w;
+    const Rec r = (Rec)u.x | ((Rec)u.y << 32);
+    link = rec_link(r); lab = rec_label(r); bpb = rec_bp_blank(r); bpn = rec_bp_nblank(r);
+  }
+}
+__global__ __launch_bounds__(256) void ctcx_traceback_seg(TraceParams tp) {
+  __shared__ __attribute__((aligned(16))) uint32_t buf[2][kTbBufBytes / 4];
+  __shared__ int32_t fbuf[2][kTbMaxG];   // (ring) the segment's frame offsets
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int rb = tp.rec_fmt == kRecFmt128 ? 16 : tp.rec_fmt == kRecFmt32 ? 4 : 8;
+  const int rw = rb >> 2;   // words per record
+  const int W = tp.W;
+  const int sl = tp.seq_len[b] > 0 ? tp.seq_len[b] : 0;
+  const int32_t* fof = tp.foff ? tp.foff + b * tp.Tmax : nullptr;
+  // frames per segment: G frames of at most W records, plus the 16-byte
+  // alignment slack, fit one buffer
+  const int G = (kTbBufBytes - 16) / (W * rb) < kTbMaxG ? (kTbBufBytes - 16) / (W * rb) : kTbMaxG;
+  const uint32_t* recw = (const uint32_t*)tp.rec;
+  const int64_t item_w = b * tp.Tmax * (int64_t)W * rw;   // the item's first word (16-byte aligned: tp.rec is)
+  // walkers
+  const bool walker = tid < 2 * tp.P;
+  const int which = tid & 1;
+  const int p = tid >> 1;
+  const int64_t bp = b * tp.P + p;
+  int32_t* const out = tp.seq + (bp * 2 + which) * tp.Tmax;
+  int len = 0, k = -1, kind = 0, prev = -1;
+  bool act = false;
+  if (walker) {
+    k = tp.top_pos[bp];
+    act = sl > 0 && k >= 0 && p < tp.item[b].n_leaves;
+    if (which == 1) {
+      kind = tp.top_kind[bp];
+      act = act && kind >= 0;
+    }
+  }
+  // the segment below frame hi: frames [lo, hi] and words [a0, a1) of the
+  // stream (absolute, a0 aligned down to 16 bytes).  [t][W]: G frames.  The
+  // record ring: each flush appends its frames newest first (ring_flush), so
+  // a flush's frames lie in one block at offsets that grow as t falls, and
+  // the block of the flush before starts lower; a segment is the frames of
+  // one block (of up to 256 and G frames) -- thread j tests frame hi - j
+  __shared__ int seg_len;
+  auto seg = [&](int hi_, int& lo, int& hi, int64_t& a0, int64_t& a1) {
+    hi = hi_;
+    int64_t w0, w1;
+    if (fof) {
+      if (tid == 0) seg_len = 256 < G ? 256 : G;
+      __syncthreads();
+      const int t = hi - tid;
+      const int fh = fof[hi];
+      bool stop = t < 0;
+      if (!stop && tid > 0)
+        stop = fof[t] < fof[t + 1] || ((int64_t)fof[t] + W - fh) * rb > kTbBufBytes - 16;
+      if (stop && tid < 256) __hip_atomic_fetch_min(&seg_len, tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __syncthreads();
+      lo = hi - seg_len + 1;
+      __syncthreads();   // (seg_len read by every thread before the next segment's reset)
+      w0 = (int64_t)fh * rw;
+      w1 = ((int64_t)fof[lo] + W) * rw;   // (a frame holds at most W records)
+    } else {
+      lo = hi - G + 1 > 0 ? hi - G + 1 : 0;
+      w0 = (int64_t)lo * W * rw;
+      w1 = (int64_t)(hi + 1) * W * rw;
+    }
+    a0 = (item_w + w0) & ~(int64_t)3;
+    a1 = item_w + w1;
+  };
+  uint4 ld[kTbLoads];
+  auto load = [&](int64_t a0, int64_t a1) {   // into registers; the last piece word by word (never past a1)
+#pragma unroll
+    for (int q = 0; q < kTbLoads; ++q) {
+      const int64_t w = a0 + 4 * ((int64_t)q * 256 + tid);
+      if (w + 4 <= a1) {
+        ld[q] = *(const uint4*)(recw + w);
+      } else if (w < a1) {
+        ld[q].x = recw[w];
+        ld[q].y = w + 1 < a1 ? recw[w + 1] : 0u;
+        ld[q].z = w + 2 < a1 ? recw[w + 2] : 0u;
+        ld[q].w = 0u;
+      }
+    }
+  };
+  auto store = [&](int bi, int64_t a0, int64_t a1, int lo, int hi) {
+#pragma unroll
+    for (int q = 0; q < kTbLoads; ++q) {
+      const int64_t w = a0 + 4 * ((int64_t)q * 256 + tid);
+      if (w < a1) *(uint4*)&buf[bi][4 * (q * 256 + tid)] = ld[q];
+    }
+    if (fof)
+      for (int f = lo + tid; f <= hi; f += 256) fbuf[bi][f - lo] = fof[f];
+  };
+  int lo = 0, hi = -1, lo1 = 0, hi1 = 0;
+  int64_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+  if (sl > 0) {
+    seg(sl - 1, lo, hi, a0, a1);
+    load(a0, a1);
+    store(0, a0, a1, lo, hi);
+    __syncthreads();
+  }
+  for (int s = 0; hi >= 0; ++s) {   // (block-uniform: sl is the item's)
+    const int bi = s & 1;
+    const bool more = lo > 0;
+    if (more) {   // the next segment's loads in flight during this one's walk
+      seg(lo - 1, lo1, hi1, b0, b1);
+      load(b0, b1);
+    }
+    if (act) {
+      for (int t = hi; t >= lo; --t) {
+        const int64_t wr = item_w + (fof ? (int64_t)fbuf[bi][t - lo] * rw : (int64_t)t * W * rw) + (int64_t)k * rw;
+        uint32_t link, bpb, bpn;
+        int lab;
+        tb_rec(&buf[bi][wr - a0], rb, link, lab, bpb, bpn);
+        if (which == 0) {
+          if (link & 1u) {
+            if (!tp.merge || lab != prev) out[len++] = lab;
+            prev = lab;
+          }
+          k = (int)(link >> 1);
+        } else {
+          out[len++] = kind == 0 ? tp.blank_label : lab;
+          const uint32_t q = kind == 0 ? bpb : bpn;
+          if (q >= kBpRestart) { act = false; break; }
+          k = (int)(q >> 1);
+          kind = (int)(q & 1u);
+        }
+      }
+    }
+    if (more) store(bi ^ 1, b0, b1, lo1, hi1);
+    __syncthreads();   // the next buffer written; this one free for the segment after
+    if (!more) break;
+    lo = lo1; hi = hi1; a0 = b0; a1 = b1;
+  }
+  if (walker) tp.len[((int64_t)p * 2 + which) * tp.len_stride + b] = len;
+}
+
 // Exclusive scan of lengths per (path, kind); also totals and maxima.
 // One 256-thread block per (path, kind).  res[(p*2+w)*2 + 0] = total, +1 = max.
 __global__ __launch_bounds__(256) void ctcx_scan(const int32_t* len, int64_t* off, int64_t* res, int64_t B) {
@@ -6393,6 +6554,15 @@ template hipError_t launch_row_norm<double>(const double*, const int32_t*, doubl
 hipError_t launch_traceback(const TraceParams& tp, hipStream_t s) {
   const int64_t n = tp.B * tp.P * 2;
   if (n == 0) return hipSuccess;
+  // the segmented walk (ctcx_traceback_seg) when an item's walkers fit one
+  // block and a segment holds at least one frame; CTCEXT_TRACEBACK=0
+  // (diagnostics) the one-thread-per-walk kernel
+  const int rb = tp.rec_fmt == kRecFmt128 ? 16 : tp.rec_fmt == kRecFmt32 ? 4 : 8;
+  const char* ev = getenv("CTCEXT_TRACEBACK");
+  if (2 * (int64_t)tp.P <= 256 && (int64_t)tp.W * rb <= kTbBufBytes - 16 && !(ev && ev[0] == '0')) {
+    hipLaunchKernelGGL(ctcx_traceback_seg, dim3((unsigned)tp.B), dim3(256), 0, s, tp);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(ctcx_traceback, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, tp);
   return hipGetLastError();
 }

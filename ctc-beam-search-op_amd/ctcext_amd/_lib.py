@@ -28,7 +28,7 @@ CTCEXT_FLAG_RING_MIN = 32      # testing: the record ring at 8 frames (short ite
 CTCEXT_FLAG_NO_RING = 64       # every beam record to HBM (the ring is the default for the score-table kernel)
 CTCEXT_FLAG_HELPER_STRICT = 128     # a helper hand-over timeout fails the call instead of a one-wave re-decode
 CTCEXT_FLAG_TEST_HELPER_DEAD = 256  # testing: the helper wave starts out timed out
-CTCEXT_ABI_VERSION = 5
+CTCEXT_ABI_VERSION = 6
 CTCEXT_SCORER_BASE = 0
 CTCEXT_SCORER_BIGRAM = 1
 

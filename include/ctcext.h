@@ -72,8 +72,10 @@ enum {
  * grows at its end: callers built against an older header use
  * ctcext_get_stats_sized with their sizeof.
  *   4: ctcext_stats.record_bytes, .helper     5: .helper_redecodes,
- *      ctcext_get_stats_sized, ctcext_abi_version, the HELPER_STRICT flag */
-#define CTCEXT_ABI_VERSION 5
+ *      ctcext_get_stats_sized, ctcext_abi_version, the HELPER_STRICT flag
+ *   6: ctcext_get_stats fills the ABI-4 prefix only (fields since: _sized);
+ *      ctcext_phase_counters' layout is [batch][32] */
+#define CTCEXT_ABI_VERSION 6
 
 typedef struct ctcext_decoder ctcext_decoder;
 
