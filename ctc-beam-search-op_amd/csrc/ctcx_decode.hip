@@ -5445,6 +5445,10 @@ __global__ __launch_bounds__(64) void ctcx_row_prep(const T* __restrict__ x, con
 #define CTCX_FACTS_COMPACT 768
 #endif
 constexpr int kFactsCompact = CTCX_FACTS_COMPACT;
+#ifndef CTCX_FACTS_INTERP
+#define CTCX_FACTS_INTERP 1
+#endif
+constexpr bool kFactsInterp = CTCX_FACTS_INTERP != 0;   // the top set's threshold by interpolation search
 // The (rank)-th largest of the n keys of a wave's compact list (rank <= n):
 // MSB-first radix select, 8-bit digits, a 256-bin LDS histogram per pass.
 // Every key lies in [klo, khi], so the bits above their highest differing bit
@@ -5746,12 +5750,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_
       unsigned tau = kt;
       if (n > K) {
         uint64_t lo = kt - 1u, hi = (uint64_t)kmx + 1ull;   // cnt(lo) >= cnt(kt) > K >= cnt(hi) = 0
+        // interpolation search on the counts, safeguarded by bisection: the
+        // count falls from clo at lo to chi at hi, and the next threshold aims
+        // at K + 1/2 linearly between them; a step that does not halve the
+        // bracket is followed by a bisection step (worst case twice the
+        // bisection's steps; ~24 of them over an N(0,1) row's key range,
+        // where the interpolation lands inside the gap between the K-th and
+        // (K+1)-th largest keys in a few).  Any search keeping cnt(lo) > K >=
+        // cnt(hi) ends at the same tau, and a threshold with a count of K
+        // exactly selects the same K keys, so S and xout are unchanged.
+        int clo = n, chi = 0;   // (clo: at least cnt(lo); n = cnt(kt) serves as the estimate)
+        bool bis = false;
         while (hi - lo > 1) {
-          const uint64_t mid = (lo + hi) >> 1;
+          const uint64_t span = hi - lo;
+          uint64_t mid;
+          if (!kFactsInterp || bis || clo <= chi) {
+            mid = (lo + hi) >> 1;
+          } else {
+            const float f = ((float)clo - ((float)K + 0.5f)) / (float)(clo - chi);
+            uint64_t d = (uint64_t)(f * (float)span);
+            d = d < 1 ? 1 : (d > span - 1 ? span - 1 : d);
+            mid = lo + d;
+          }
           const int c2 = cnt_ge((unsigned)mid);
-          if (c2 <= K) hi = mid;
-          else lo = mid;
+          if (c2 <= K) { hi = mid; chi = c2; }
+          else { lo = mid; clo = c2; }
           if (c2 == K) break;
+          bis = !bis && 2 * (hi - lo) > span;
         }
         tau = (unsigned)hi;
       }
