@@ -5446,7 +5446,7 @@ __global__ __launch_bounds__(64) void ctcx_row_prep(const T* __restrict__ x, con
 #endif
 constexpr int kFactsCompact = CTCX_FACTS_COMPACT;
 #ifndef CTCX_FACTS_INTERP
-#define CTCX_FACTS_INTERP 1
+#define CTCX_FACTS_INTERP 0
 #endif
 constexpr bool kFactsInterp = CTCX_FACTS_INTERP != 0;   // the top set's threshold by interpolation search
 // The (rank)-th largest of the n keys of a wave's compact list (rank <= n):
