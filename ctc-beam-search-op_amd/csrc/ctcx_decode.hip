@@ -5993,9 +5993,9 @@ __global__ __launch_bounds__(256) void ctcx_traceback(TraceParams tp) {
 // global load per frame (~1.1 us at cfg3: 1.74 ms for 1500 frames).  Two
 // buffers: the next segment's loads are in flight, in registers, while the
 // walkers step through the current one.
-// (static LDS stays within the 64 KB a plain launch gets: two 24-KB buffers
-// and the offsets, 56 KB -- at 72 KB the launch ran with 64 and the offsets
-// past it read as 0)
+// (static LDS stays within the 64 KB a plain launch gets without an
+// attribute: two 24-KB buffers and the offsets, 56 KB; a first 72-KB version
+// was cut to this while its real fault, the ring's frame order, was found)
 constexpr int kTbBufBytes = 24 * 1024;           // one segment buffer
 constexpr int kTbLoads = kTbBufBytes / 16 / 256;  // 16-byte loads per thread per segment
 static_assert(kTbLoads * 16 * 256 == kTbBufBytes, "whole loads");
