@@ -1701,6 +1701,18 @@ __device__ __forceinline__ void wsync() {
 #ifndef CTCX_SLEEP
 #define CTCX_SLEEP 1
 #endif
+// CTCX_RDY_TRIP=1: a chunk hand-over read as one LDS round trip (the count's
+// readfirstlane after the slot's words complete, not before they are issued).
+// Local ISA change, measured slower on the same box (cfg3 +0.2%, cfg4 +0.1%,
+// cfg2 +0.3%, cfg5 +0.2%; profiles/r6h_ab_rdy_trip.txt): off
+#ifndef CTCX_RDY_TRIP
+#define CTCX_RDY_TRIP 0
+#endif
+#if CTCX_RDY_TRIP
+#define CTCX_ONE_TRIP(rdy, ...) __asm__ volatile("" : "+v"(rdy) : __VA_ARGS__)
+#else
+#define CTCX_ONE_TRIP(rdy, ...) __asm__ volatile("" ::__VA_ARGS__)
+#endif
 constexpr int kTabSlots = CTCX_TAB_SLOTS;   // chunk slots in the ring
 // A hand-over wait gives up after ~1 s of the constant 100 MHz clock
 // (s_memrealtime), whatever the shader clock or the SIMD's other work: only a
@@ -2751,15 +2763,16 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
             // one batch of reads, no loop around it (a loop would make the
             // compiler wait out every read's predecessor: write-after-write on
             // the same registers across the back edge)
-            const int rdy = __hip_atomic_load(&cx.misc[kCtlReady], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            int rdy = __hip_atomic_load(&cx.misc[kCtlReady], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             __asm__ volatile("" ::: "memory");
             ta[0] = tb.a[s0];
             tpv[0] = tb.p[s0];
             ta[1] = tb.a[s1];
             tpv[1] = tb.p[s1];
             // the slot reads complete with the count (one round trip): otherwise
-            // the compiler sinks them below the test, a second round trip
-            __asm__ volatile("" ::"v"(ta[0]), "v"(ta[1]), "v"(tpv[0]), "v"(tpv[1]));
+            // the compiler sinks them below the test, or hoists the count's
+            // readfirstlane above them -- a second round trip either way
+            CTCX_ONE_TRIP(rdy, "v"(ta[0]), "v"(ta[1]), "v"(tpv[0]), "v"(tpv[1]));
             if (__builtin_expect(uni(rdy) < need, 0)) {
               // wave 1 is behind (rare): wait for the count, then read again.
               // A wait that runs out of time, or a helper that gave up, ends
@@ -3088,13 +3101,13 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
         };
         {
           // one batch of reads, no loop around it (see the score-table read)
-          const int rdy = __hip_atomic_load(&cx.misc[kCtlReady], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          int rdy = __hip_atomic_load(&cx.misc[kCtlReady], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           __asm__ volatile("" ::: "memory");
           read_slot();
           if constexpr (SQ)
-            __asm__ volatile("" ::"v"(h0), "v"(h1), "v"(h2), "v"(h3), "v"(gqa), "v"(gqv), "v"(gqp));   // one round trip
+            CTCX_ONE_TRIP(rdy, "v"(h0), "v"(h1), "v"(h2), "v"(h3), "v"(gqa), "v"(gqv), "v"(gqp));   // one round trip
           else
-            __asm__ volatile("" ::"v"(h0), "v"(h1), "v"(h2), "v"(h3), "v"(gqe), "v"(gqp));
+            CTCX_ONE_TRIP(rdy, "v"(h0), "v"(h1), "v"(h2), "v"(h3), "v"(gqe), "v"(gqp));
           if (__builtin_expect(uni(rdy) <= gqc && !cx.tabdead, 0)) {
             // wave 1 is behind: wait for the count, then read again (a wait that
             // runs out of time, or a helper that gave up, takes cqn = 0 below:
