@@ -284,11 +284,16 @@ struct Ctx {
 };
 // the helper wave's phase counters (diagnostics build): lane 0 of wave 1 adds
 #ifdef CTCX_PHASES
-#define CTCX_HPC(cx, i, v)                                                                              \
+#define CTCX_HPC_(cx, i, v)                                                                             \
   do {                                                                                                  \
     if ((cx).prof && threadIdx.x == 64)                                                                 \
       __hip_atomic_fetch_add((cx).prof + (i), (uint64_t)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); \
   } while (0)
+#ifdef CTCX_PHASE_TIES   // (the helper's counters carry the tie diagnostics only)
+#define CTCX_HPC(cx, i, v) do { } while (0)
+#else
+#define CTCX_HPC(cx, i, v) CTCX_HPC_(cx, i, v)
+#endif
 #define CTCX_HTIME() __builtin_amdgcn_s_memtime()
 #else
 #define CTCX_HPC(cx, i, v) do { } while (0)
@@ -2438,7 +2443,7 @@ constexpr bool kExtBig = CTCX_EXT_BIG != 0;   // large C too: off (cfg4 162.5 ->
 constexpr int kCtlStop = 3, kCtlExt = 7;   // (misc words; both reset per frame)
 constexpr int kExtMinW = 16;               // beams below this pop too few positions to gain
 template <typename T>
-__device__ __forceinline__ void help_rank_extract(const Ctx<T>& cx) {
+__device__ __forceinline__ void help_rank_extract(const Ctx<T>& cx, int tbuf = 0) {
   const int lane = threadIdx.x & 63;
   CTCX_LDS int* m = cx.misc;
   if (ctl_ld(m, kCtlDead) != 0) return;
@@ -2476,6 +2481,32 @@ __device__ __forceinline__ void help_rank_extract(const Ctx<T>& cx) {
   if (in0 && e0 > 1) p = g0 < p ? g0 : p;
   if (in1 && e1 > 1) p = g1 < p ? g1 : p;
   p = uni(wave_min(p));
+#ifdef CTCX_PHASE_EXTP   // (diagnostics: the stop the helper found, 16-bit frame counts per range)
+  CTCX_HPC(cx, 27, 1ull << (16 * (p <= 2 ? 0 : p < 64 ? 1 : p < 96 ? 2 : 3)));
+#endif
+#ifdef CTCX_PHASE_TIES   // (diagnostics: what the first two entries tied at rank p are)
+  if (p < W) {
+    const uint64_t t0m = __ballot(in0 && e0 > 1 && g0 == p), t1m = __ballot(in1 && e1 > 1 && g1 == p);
+    const int fa = t0m ? (int)__builtin_ctzll(t0m) : 64 + (int)__builtin_ctzll(t1m);
+    const uint64_t r0 = fa < 64 ? (t0m & (t0m - 1)) : 0ull, r1 = fa < 64 ? t1m : (t1m & (t1m - 1));
+    const int fb = r0 ? (int)__builtin_ctzll(r0) : 64 + (int)__builtin_ctzll(r1);
+    const int sa = cx.alias[fa], sb = cx.alias[fb];
+    const uint32_t ka = cx.ekind[sa], kb = cx.ekind[sb];
+    const int l = cx.elab[sa];
+    if ((ka & 1u) && (kb & 1u) && l == cx.elab[sb]) {   // two new children, one label: their parents
+      const int pa = (int)(ka >> 1), pb = (int)(kb >> 1);
+      const int la = sel(cx.lab, tbuf)[pa], lb = sel(cx.lab, tbuf)[pb];
+      const int qa = sel(cx.par, tbuf)[pa], qb = sel(cx.par, tbuf)[pb];
+      CTCX_HPC_(cx, 25, 1);
+      CTCX_HPC_(cx, 29, (l == la) + (l == lb));
+      CTCX_HPC_(cx, 30, (qa == pb || qb == pa) ? 1 : 0);
+      CTCX_HPC_(cx, 27, qa == qb ? 1 : 0);
+      CTCX_HPC_(cx, 26, la == lb ? 1 : 0);
+      CTCX_HPC_(cx, 24, sel(cx.ot, tbuf)[pa] == sel(cx.ot, tbuf)[pb] ? 1 : 0);
+      CTCX_HPC_(cx, 31, (sel(cx.ob, tbuf)[pa] == sel(cx.ot, tbuf)[pb] || sel(cx.ob, tbuf)[pb] == sel(cx.ot, tbuf)[pa]) ? 1 : 0);
+    }
+  }
+#endif
   if (p <= 2) return;   // wave 0 pops every position anyway
   if (in0 && g0 < p) cx.sorted[g0] = cx.alias[lane];
   if (in1 && g1 < p) cx.sorted[g1] = cx.alias[lane + 64];
@@ -2593,7 +2624,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
         if (nb >= W) help_gather_scored<T, BIG>(cx, gq, buf, nb, norm, pmax, wave_min(lmin));
         if constexpr (RN == 1 && kExtRank && (kExtBig || !BIG) && !kExtLate) {
           [[maybe_unused]] const uint64_t hr0 = CTCX_HTIME();
-          help_rank_extract<T>(cx);
+          help_rank_extract<T>(cx, buf);
           CTCX_HPC(cx, 28, CTCX_HTIME() - hr0);
         }
       } else if constexpr (BIG) {
@@ -3748,6 +3779,9 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     int fs = front.s;
     int srt0 = 0, srt1 = 0;
     int stop = 2;   // positions below it: placed by rank (help_rank_extract)
+#ifdef CTCX_PHASE_EXTP
+    int ext_pops = 0;
+#endif
     if constexpr (sizeof(T) == 4) {
       const unsigned heb = (unsigned)(uintptr_t)he;
       const unsigned aj = heb + 8u * (unsigned)(lane + 1), al = heb + 8u * (unsigned)(2 * lane + 2);
@@ -3760,6 +3794,9 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
         const int hi = W < top ? W : top;
         const int l = lo > stop ? lo : stop;
         if (hi > l) extract_f32(heb, uni(hi), uni(l), base, geo.anc, geo.req, aj, al, ar, dum, srt, fs);
+#ifdef CTCX_PHASE_EXTP
+        if (hi > l) ext_pops += hi - l;
+#endif
       };
       auto poll = [&]() {
         if (ext_rank) {   // acquire: the helper's sorted[] writes before its release of kCtlStop
@@ -3792,6 +3829,9 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
         fs = keep ? uni(v.s) : s0;
       }
     }
+#ifdef CTCX_PHASE_EXTP   // (diagnostics: the stop wave 0 used, and the frames it came from the helper)
+    if (pc) { pc[16] += stop; pc[17] += stop > 2 ? 1 : 0; pc[18] += ext_pops; }
+#endif
     // pop_heap(2): the front goes to position 1, e[1] becomes the root
     if (stop <= 2) {
       srt0 = writelane(srt0, fs, 1);

@@ -64,3 +64,17 @@ for k, name in hn.items():
     print("  %-26s %10.0f cycles/frame" % (name, m[k] / fr))
 print("  helper chunks %.2f/frame, scan steps %.2f/frame, child-walk steps %.2f/frame"
       % (m[30] / fr, m[31] / fr, m[27] / fr))
+if os.environ.get("CTCX_DIAG_EXTP"):   # (a build with -DCTCX_PHASE_EXTP: the extract's stop)
+    h = buf[:, 27].astype(np.uint64)
+    cnt = [int(((h >> np.uint64(16 * k)) & np.uint64(0xFFFF)).sum()) for k in range(4)]
+    nf = max(1, sum(cnt))
+    print("  (raw helper words, items 0-3: %s)" % [hex(int(v)) for v in h[:4]])
+    print("  extract stop (helper): p<=2 %.3f, 3..63 %.3f, 64..95 %.3f, 96..128 %.3f of %d frames" % (
+        cnt[0] / nf, cnt[1] / nf, cnt[2] / nf, cnt[3] / nf, nf))
+    print("  extract: wave 0's stop mean %.1f, frames with a helper stop %.3f, pops %.1f per frame" % (
+        m[16] / fr, m[17] / fr, m[18] / fr))
+if os.environ.get("CTCX_DIAG_TIES"):   # (a build with -DCTCX_PHASE_TIES: the first tied pair at rank p)
+    nt = max(1.0, m[25])
+    print("  ties (two new children, one label): %.3f of frames; parents: label = child's (sum of 2) %.3f,"
+          " one the other's parent %.3f, siblings %.3f, same label %.3f, equal totals %.3f, blank = other's total %.3f"
+          % (m[25] / fr, m[29] / nt, m[30] / nt, m[27] / nt, m[26] / nt, m[24] / nt, m[31] / nt))
