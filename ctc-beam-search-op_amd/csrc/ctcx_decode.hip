@@ -289,7 +289,7 @@ struct Ctx {
     if ((cx).prof && threadIdx.x == 64)                                                                 \
       __hip_atomic_fetch_add((cx).prof + (i), (uint64_t)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); \
   } while (0)
-#ifdef CTCX_PHASE_TIES   // (the helper's counters carry the tie diagnostics only)
+#if defined(CTCX_PHASE_TIES) || defined(CTCX_PHASE_EXTT)   // (the helper's counters carry those diagnostics only)
 #define CTCX_HPC(cx, i, v) do { } while (0)
 #else
 #define CTCX_HPC(cx, i, v) CTCX_HPC_(cx, i, v)
@@ -1718,6 +1718,19 @@ __device__ __forceinline__ void wsync() {
 #else
 #define CTCX_ONE_TRIP(rdy, ...) __asm__ volatile("" ::__VA_ARGS__)
 #endif
+// CTCX_HELPER_CALL=1: the helper wave's gather and rank functions as real
+// calls (Ctx by value, as literal_step), so their code is allocated apart from
+// wave 0's frame loop
+#ifndef CTCX_HELPER_CALL
+#define CTCX_HELPER_CALL 0
+#endif
+#if CTCX_HELPER_CALL
+#define CTCX_HELPER_FN __attribute__((noinline))
+#define CTCX_HCTX Ctx<T>
+#else
+#define CTCX_HELPER_FN __forceinline__
+#define CTCX_HCTX const Ctx<T>&
+#endif
 constexpr int kTabSlots = CTCX_TAB_SLOTS;   // chunk slots in the ring
 // A hand-over wait gives up after ~1 s of the constant 100 MHz clock
 // (s_memrealtime), whatever the shader clock or the SIMD's other work: only a
@@ -2324,7 +2337,7 @@ constexpr bool kSqFirst1 = CTCX_SQ_FIRST1 != 0;
 #endif
 constexpr int kSqCap0 = CTCX_SQ_CAP0;   // large C: offers in the frame's first chunk (cfg4: 16, 32, 64 within 0.2%)
 template <typename T, bool BIG>
-__device__ __forceinline__ void help_gather_scored(const Ctx<T>& cx, GQ q, int buf, int nb, T norm, T pmax,
+__device__ CTCX_HELPER_FN void help_gather_scored(CTCX_HCTX cx, GQ q, int buf, int nb, T norm, T pmax,
                                                    T bottom) {
   const int lane = threadIdx.x & 63;
   CTCX_LDS int* m = cx.misc;
@@ -2438,12 +2451,23 @@ constexpr bool kExtRank = CTCX_EXT_RANK != 0;
 #ifndef CTCX_EXT_LATE
 #define CTCX_EXT_LATE 0
 #endif
-constexpr bool kExtLate = CTCX_EXT_LATE != 0;   // (A/B: the helper ranks after its pending ring flush)
+constexpr bool kExtLate = CTCX_EXT_LATE != 0;
+// CTCX_RANK_FAST: the helper ranks by ">" alone and finds ties by collision
+// (half the compares); CTCX_EXT_FIRST > 0: wave 0 reads the helper's stop
+// after its first CTCX_EXT_FIRST pops, not only after the first 32
+#ifndef CTCX_RANK_FAST
+#define CTCX_RANK_FAST 0
+#endif
+#ifndef CTCX_EXT_FIRST
+#define CTCX_EXT_FIRST 0
+#endif
+constexpr bool kRankFast = CTCX_RANK_FAST != 0;
+constexpr int kExtFirst = CTCX_EXT_FIRST;   // (A/B: the helper ranks after its pending ring flush)
 constexpr bool kExtBig = CTCX_EXT_BIG != 0;   // large C too: off (cfg4 162.5 -> 169.6 ms, same box; cfg3 unmoved)
 constexpr int kCtlStop = 3, kCtlExt = 7;   // (misc words; both reset per frame)
 constexpr int kExtMinW = 16;               // beams below this pop too few positions to gain
 template <typename T>
-__device__ __forceinline__ void help_rank_extract(const Ctx<T>& cx, int tbuf = 0) {
+__device__ CTCX_HELPER_FN void help_rank_extract(CTCX_HCTX cx, CTCX_LDS int* scr, int tbuf = 0) {
   const int lane = threadIdx.x & 63;
   CTCX_LDS int* m = cx.misc;
   if (ctl_ld(m, kCtlDead) != 0) return;
@@ -2459,25 +2483,55 @@ __device__ __forceinline__ void help_rank_extract(const Ctx<T>& cx, int tbuf = 0
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   if (ctl_ld(m, kCtlExt) != 1) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#ifdef CTCX_PHASE_EXTT
+  const uint32_t hx0 = (uint32_t)__builtin_amdgcn_s_memtime();
+  CTCX_HPC_(cx, 24, hx0 - (uint32_t)m[14]);   // (kCtlDone seen, after wave 0's extract start)
+#endif
   const int W = cx.W;
   const CTCX_LDS float* xv = (const CTCX_LDS float*)cx.newpos;
   const bool in0 = lane < W, in1 = lane + 64 < W;
   const float v0 = in0 ? xv[lane] : 0.0f, v1 = in1 ? xv[lane + 64] : 0.0f;
   int g0 = 0, e0 = 0, g1 = 0, e1 = 0;
   const int W4 = (W + 3) >> 2;   // (wave 0 pads the copy to a multiple of 4 with NaN: never > or ==)
-  for (int j = 0; j < W4; ++j) {
-    const u32x4 xq = ((const CTCX_LDS u32x4*)xv)[j];   // one address: a broadcast
-    const float x[4] = {__uint_as_float(xq.x), __uint_as_float(xq.y), __uint_as_float(xq.z), __uint_as_float(xq.w)};
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      g0 += x[u] > v0;
-      e0 += x[u] == v0;
-      g1 += x[u] > v1;
-      e1 += x[u] == v1;
-    }
-  }
-  if (__ballot((in0 && v0 != v0) || (in1 && v1 != v1))) return;   // (no order to rank by)
   int p = W;
+  if constexpr (kRankFast) {
+    // ranks by ">" alone (equal totals share a rank, distinct ones never do),
+    // the broadcast reads batched ahead of the compares
+#pragma unroll 8
+    for (int j = 0; j < W4; ++j) {
+      const u32x4 xq = ((const CTCX_LDS u32x4*)xv)[j];
+      const float x[4] = {__uint_as_float(xq.x), __uint_as_float(xq.y), __uint_as_float(xq.z), __uint_as_float(xq.w)};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        g0 += x[u] > v0;
+        g1 += x[u] > v1;
+      }
+    }
+    if (__ballot((in0 && v0 != v0) || (in1 && v1 != v1))) return;   // (no order to rank by)
+    // a tie is two entries of one rank: each entry writes its index at its
+    // rank in scr (the gather queue's score plane: free once the grow is
+    // over), and of two that collide at least one reads back the other's
+    if (in0) scr[g0] = lane;
+    if (in1) scr[g1] = lane + 64;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    e0 = (in0 && scr[g0] != lane) ? 2 : 1;
+    e1 = (in1 && scr[g1] != lane + 64) ? 2 : 1;
+  } else {
+    for (int j = 0; j < W4; ++j) {
+      const u32x4 xq = ((const CTCX_LDS u32x4*)xv)[j];   // one address: a broadcast
+      const float x[4] = {__uint_as_float(xq.x), __uint_as_float(xq.y), __uint_as_float(xq.z), __uint_as_float(xq.w)};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        g0 += x[u] > v0;
+        e0 += x[u] == v0;
+        g1 += x[u] > v1;
+        e1 += x[u] == v1;
+      }
+    }
+    if (__ballot((in0 && v0 != v0) || (in1 && v1 != v1))) return;   // (no order to rank by)
+  }
   if (in0 && e0 > 1) p = g0 < p ? g0 : p;
   if (in1 && e1 > 1) p = g1 < p ? g1 : p;
   p = uni(wave_min(p));
@@ -2511,10 +2565,15 @@ __device__ __forceinline__ void help_rank_extract(const Ctx<T>& cx, int tbuf = 0
   if (in0 && g0 < p) cx.sorted[g0] = cx.alias[lane];
   if (in1 && g1 < p) cx.sorted[g1] = cx.alias[lane + 64];
   __hip_atomic_store(&m[kCtlStop], p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef CTCX_PHASE_EXTT   // (diagnostics: cycles from wave 0's extract start to this publish)
+  CTCX_HPC_(cx, 25, (uint32_t)__builtin_amdgcn_s_memtime() - (uint32_t)m[14]);
+  CTCX_HPC_(cx, 26, 1);
+  CTCX_HPC_(cx, 27, (uint32_t)__builtin_amdgcn_s_memtime() - hx0);
+#endif
 }
 
 template <typename T>
-__device__ __forceinline__ void help_gather_chunks(const Ctx<T>& cx, GQ q, int buf, int nb, T norm, T pmax, T bottom,
+__device__ CTCX_HELPER_FN void help_gather_chunks(CTCX_HCTX cx, GQ q, int buf, int nb, T norm, T pmax, T bottom,
                                                    int lead) {
   const int lane = threadIdx.x & 63;
   CTCX_LDS int* m = cx.misc;
@@ -2624,7 +2683,7 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
         if (nb >= W) help_gather_scored<T, BIG>(cx, gq, buf, nb, norm, pmax, wave_min(lmin));
         if constexpr (RN == 1 && kExtRank && (kExtBig || !BIG) && !kExtLate) {
           [[maybe_unused]] const uint64_t hr0 = CTCX_HTIME();
-          help_rank_extract<T>(cx, buf);
+          help_rank_extract<T>(cx, (CTCX_LDS int*)gq.p, buf);
           CTCX_HPC(cx, 28, CTCX_HTIME() - hr0);
         }
       } else if constexpr (BIG) {
@@ -3790,10 +3849,21 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       // positions 127..64 into srt1, 63..2 into srt0, in four segments; with
       // the helper ranking (ext_rank), kCtlStop is read between them and the
       // pops end at the first position it has not placed
+#ifdef CTCX_PHASE_EXTT
+      if (lane == 0) cx.misc[14] = (int)(uint32_t)__builtin_amdgcn_s_memtime();
+#endif
+      int cur = W;   // the next position to pop, plus one
       auto seg = [&](int top, int lo, int base, int& srt) {
-        const int hi = W < top ? W : top;
+        const int hi = cur < top ? cur : top;
         const int l = lo > stop ? lo : stop;
+        if constexpr (kExtFirst > 0) cur = hi > l ? l : cur;   // (the segments run in order, contiguous)
+#ifdef CTCX_PHASE_EXTT
+        const uint64_t sx0 = __builtin_amdgcn_s_memtime();
+#endif
         if (hi > l) extract_f32(heb, uni(hi), uni(l), base, geo.anc, geo.req, aj, al, ar, dum, srt, fs);
+#ifdef CTCX_PHASE_EXTT
+        if (pc && hi > l) { pc[23] += __builtin_amdgcn_s_memtime() - sx0; pc[17] += 1; pc[18] += hi - l; }
+#endif
 #ifdef CTCX_PHASE_EXTP
         if (hi > l) ext_pops += hi - l;
 #endif
@@ -3806,6 +3876,14 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
       };
       // (polls every 16 or 8 pops measured slower: cfg3 +0.4% / +1.2%,
       // profiles/r6i_ab_ext_seg.txt -- the helper's stop rarely lands early)
+      if constexpr (kExtFirst > 0) {
+        if (ext_rank) {   // the first kExtFirst pops, then a poll (uniform)
+          const int f1 = W - kExtFirst > 2 ? W - kExtFirst : 2;
+          seg(128, f1 > 64 ? f1 : 64, 64, srt1);
+          seg(64, f1, 0, srt0);
+          poll();
+        }
+      }
       seg(128, 96, 64, srt1);
       poll();
       seg(96, 64, 64, srt1);
@@ -4684,7 +4762,7 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
         CTCX_HPC(cx, 29, CTCX_HTIME() - hf0);
       }
       if constexpr (SQ && RN == 1 && kExtRank && (kExtBig || !BIG) && kExtLate)
-        if (helper_wave()) help_rank_extract<T>(cx);
+        if (helper_wave()) help_rank_extract<T>(cx, (CTCX_LDS int*)gq.p);
       pf_t = -1;
       __syncthreads();
       why = uni(cx.misc[4]);

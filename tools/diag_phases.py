@@ -78,3 +78,11 @@ if os.environ.get("CTCX_DIAG_TIES"):   # (a build with -DCTCX_PHASE_TIES: the fi
     print("  ties (two new children, one label): %.3f of frames; parents: label = child's (sum of 2) %.3f,"
           " one the other's parent %.3f, siblings %.3f, same label %.3f, equal totals %.3f, blank = other's total %.3f"
           % (m[25] / fr, m[29] / nt, m[30] / nt, m[27] / nt, m[26] / nt, m[24] / nt, m[31] / nt))
+if os.environ.get("CTCX_DIAG_EXTT"):   # (a build with -DCTCX_PHASE_EXTT: when the helper's stop lands)
+    print("  extract: helper stop published in %.3f of frames, %.0f cycles after wave 0's extract start;"
+          " asm segments %.2f per frame, %.1f pops, %.0f cycles in them (%.0f per pop), extract phase %.0f"
+          % (m[26] / fr, m[25] / max(1.0, m[26]), m[17] / fr, m[18] / fr, m[23] / fr, m[23] / max(1.0, m[18]), m[3] / fr))
+if os.environ.get("CTCX_DIAG_EXTT"):
+    print("  helper: kCtlDone seen %.0f cycles after wave 0's extract start (all frames it ranks), rank to publish %.0f"
+          % (m[24] / max(1.0, m[26]), m[27] / max(1.0, m[26])))
+
