@@ -157,6 +157,47 @@ __device__ __forceinline__ float row16_fmax_dpp(float v) {
       : "+v"(v));
   return v;
 }
+// The set mode's beam (kSetMode): W <= 128 (value, slot) pairs, position j in
+// lane j & 63 of (sv0, ss0) for j < 64, of (sv1, ss1) above; +inf past W.
+__device__ __forceinline__ float row16_fmin_dpp(float v) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_min_f32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_min_f32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_min_f32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_min_f32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf"
+      : "+v"(v));
+  return v;
+}
+// position loc (uniform) := (v, s)
+__device__ __forceinline__ void set_put(float& sv0, int& ss0, float& sv1, int& ss1, int loc, float v, int s) {
+  const bool me = (int)(threadIdx.x & 63) == (loc & 63);
+  if (loc < 64) {
+    sv0 = me ? v : sv0;
+    ss0 = me ? s : ss0;
+  } else {
+    sv1 = me ? v : sv1;
+    ss1 = me ? s : ss1;
+  }
+}
+// the set's minimum (fv), its slot (fs) and position (loc), and whether another
+// position holds the same value (tied: which of them a heap would evict
+// depends on its layout).  Values are finite, never NaN.
+__device__ __forceinline__ void set_front(float sv0, int ss0, float sv1, int ss1, float& fv, int& fs, int& loc,
+                                          bool& tied) {
+  const float r = row16_fmin_dpp(__builtin_fminf(sv0, sv1));
+  const float a = bcast(r, 15), b = bcast(r, 31), c = bcast(r, 47), d = bcast(r, 63);
+  const float mm = __builtin_fminf(__builtin_fminf(a, b), __builtin_fminf(c, d));
+  const uint64_t e0 = __ballot(sv0 == mm), e1 = __ballot(sv1 == mm);
+  tied = (__builtin_popcountll(e0) + __builtin_popcountll(e1)) > 1;
+  const int l0 = (int)__builtin_ctzll(e0), l1 = (int)__builtin_ctzll(e1);
+  loc = e0 ? l0 : 64 + l1;
+  fs = e0 ? __builtin_amdgcn_readlane(ss0, l0) : __builtin_amdgcn_readlane(ss1, l1);
+  fv = mm;
+}
 // the same by v_max_f32 (IEEE maxNum: a NaN operand loses; of +0 and -0
 // either may come back) -- for maxima whose zero sign nothing reads (the row
 // facts' maxima: compared, or subtracted from values as a softmax maximum)
@@ -289,7 +330,7 @@ struct Ctx {
     if ((cx).prof && threadIdx.x == 64)                                                                 \
       __hip_atomic_fetch_add((cx).prof + (i), (uint64_t)(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); \
   } while (0)
-#if defined(CTCX_PHASE_TIES) || defined(CTCX_PHASE_EXTT)   // (the helper's counters carry those diagnostics only)
+#if defined(CTCX_PHASE_TIES) || defined(CTCX_PHASE_EXTT) || defined(CTCX_PHASE_BIRTH)   // (the helper's counters carry those diagnostics only)
 #define CTCX_HPC(cx, i, v) do { } while (0)
 #else
 #define CTCX_HPC(cx, i, v) CTCX_HPC_(cx, i, v)
@@ -1164,6 +1205,133 @@ __device__ __forceinline__ int heap_events_f32(float s, int c, int sl, unsigned 
       : "memory", "vcc", "m0", "s80", "s81", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93",
         "s94", "s95", "s96", "s97", "s98", "s99", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239",
         "v240", "v241", "v242", "v243");
+  return st;
+}
+
+// The set mode's event loop (kSetMode, exact_step): heap_events_f32's
+// selections and bookkeeping, with the push a register write at the front's
+// position (floc) and the new front a DPP minimum over the set (row shifts,
+// then row_bcast 15 / 31: the minimum lands in lane 63), its position and slot
+// by ballot.  Returns 0 (no live lane wants in), 1 (lane k re-offers a branch
+// child: the caller decides it) or 2 (the next eviction meets equal minima,
+// ftied: which one a heap evicts depends on its layout -- replay).
+// Temporaries: s80..s81, s84..s96, vcc, m0, v232, v242.
+__device__ __forceinline__ int set_events_f32(float s, int c, int sl, float& sv0, int& ss0, float& sv1, int& ss1,
+                                              int& myslot, int& evr, float& bat, uint64_t& NC, uint64_t& RB,
+                                              uint64_t& done, uint64_t LB, float& fv, int& fs, int& floc, int& ftied,
+                                              int& nfree, int& nv, int nb, int& k, int& cnt) {
+  int st;
+  NC = uni64(NC); RB = uni64(RB); done = uni64(done); LB = uni64(LB);
+  fv = uni(fv); fs = uni(fs); floc = uni(floc); ftied = uni(ftied); nfree = uni(nfree); nv = uni(nv); nb = uni(nb);
+  cnt = uni(cnt);
+  asm volatile(
+      "s_mov_b32 %[st], 0\n\t"
+      "s_not_b64 s[80:81], %[done]\n\t"                    // lanes still to come
+      "v_cmp_lt_f32_e64 s[88:89], %[fv], %[s]\n\t"          // s > front
+      "s_and_b64 s[88:89], s[88:89], %[nc]\n\t"
+      "s_or_b64 s[88:89], s[88:89], %[rb]\n\t"
+      "s_and_b64 s[88:89], s[88:89], s[80:81]\n\t"         // m (SCC: m != 0)
+      "s_cbranch_scc0 .Lse_exit_%=\n\t"
+      "s_ff1_i32_b64 %[k], s[88:89]\n\t"
+      "s_bitcmp1_b64 %[lb], %[k]\n\t"
+      "s_cbranch_scc1 .Lse_rare_%=\n"
+      ".Lse_tail_%=:\n\t"
+      "s_cmp_lg_u32 %[ft], 0\n\t"                          // equal minima: the eviction is the heap's
+      "s_cbranch_scc1 .Lse_tie_%=\n\t"
+      "s_lshl_b64 s[80:81], -2, %[k]\n\t"                  // lanes after k
+      "v_readlane_b32 s84, %[s], %[k]\n\t"                 // v = offer k's score
+      "s_mov_b32 s85, %[fs]\n\t"                           // slot = the front's
+      "s_cmp_lt_i32 %[fs], %[nb]\n\t"
+      "s_cbranch_scc1 .Lse_evb_%=\n"
+      ".Lse_slot_%=:\n\t"
+      "v_cmp_eq_u32_e64 s[90:91], %[fs], %[my]\n\t"        // an entry accepted in this chunk is the evicted front
+      "s_mov_b32 m0, %[k]\n\t"
+      "v_cndmask_b32_e64 %[my], %[my], -1, s[90:91]\n\t"
+      "v_writelane_b32 %[my], s85, m0\n\t"                 // lane k: its entry's slot
+      CTCX_EVCNT
+      "s_and_b32 m0, %[floc], 63\n\t"                      // (v, slot) replaces the front
+      "s_cmp_lt_u32 %[floc], 64\n\t"
+      "s_cbranch_scc0 .Lse_put1_%=\n\t"
+      "v_writelane_b32 %[sv0], s84, m0\n\t"
+      "v_writelane_b32 %[ss0], s85, m0\n\t"
+      "s_branch .Lse_min_%=\n"
+      ".Lse_put1_%=:\n\t"
+      "v_writelane_b32 %[sv1], s84, m0\n\t"
+      "v_writelane_b32 %[ss1], s85, m0\n"
+      ".Lse_min_%=:\n\t"
+      "s_nop 1\n\t"
+      "v_min_f32_e32 v232, %[sv0], %[sv1]\n\t"
+      "s_nop 1\n\t"
+      "v_min_f32_dpp v232, v232, v232 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_min_f32_dpp v232, v232, v232 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_min_f32_dpp v232, v232, v232 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_min_f32_dpp v232, v232, v232 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_min_f32_dpp v232, v232, v232 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_min_f32_dpp v232, v232, v232 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_readlane_b32 %[fv], v232, 63\n\t"                 // the new front's value
+      "s_nop 1\n\t"
+      "v_cmp_eq_f32_e64 s[86:87], %[fv], %[sv0]\n\t"       // its positions
+      "v_cmp_eq_f32_e64 s[92:93], %[fv], %[sv1]\n\t"
+      "s_bcnt1_i32_b64 s94, s[86:87]\n\t"
+      "s_bcnt1_i32_b64 s95, s[92:93]\n\t"
+      "s_add_u32 s94, s94, s95\n\t"
+      "s_cmp_gt_u32 s94, 1\n\t"
+      "s_cselect_b32 %[ft], 1, 0\n\t"
+      "s_ff1_i32_b64 s94, s[86:87]\n\t"
+      "s_ff1_i32_b64 s95, s[92:93]\n\t"
+      "s_cmp_lg_u64 s[86:87], 0\n\t"
+      "s_cbranch_scc0 .Lse_loc1_%=\n\t"
+      "s_mov_b32 %[floc], s94\n\t"
+      "v_readlane_b32 %[fs], %[ss0], s94\n\t"
+      "s_branch .Lse_locd_%=\n"
+      ".Lse_loc1_%=:\n\t"
+      "s_add_u32 %[floc], s95, 64\n\t"
+      "v_readlane_b32 %[fs], %[ss1], s95\n"
+      ".Lse_locd_%=:\n\t"
+      "v_cmp_lt_i32_e64 vcc, %[k], %[sl]\n\t"              // turns starting after lane k see the new bottom
+      "v_mov_b32_e32 v242, %[fv]\n\t"
+      "v_cndmask_b32_e32 %[bat], %[bat], v242, vcc\n\t"
+      "v_cmp_lt_f32_e64 s[88:89], %[fv], %[s]\n\t"         // next: s > front
+      "s_and_b64 s[88:89], s[88:89], %[nc]\n\t"
+      "s_or_b64 s[88:89], s[88:89], %[rb]\n\t"
+      "s_and_b64 s[88:89], s[88:89], s[80:81]\n\t"         // next m
+      "s_cbranch_scc0 .Lse_exit_%=\n\t"
+      "s_ff1_i32_b64 %[k], s[88:89]\n\t"
+      "s_bitcmp1_b64 %[lb], %[k]\n\t"
+      "s_cbranch_scc0 .Lse_tail_%=\n\t"                    // the next push, unless k is rare
+      "s_branch .Lse_rare_%=\n"
+      // the evicted front is a branch's entry: a fresh slot; record the
+      // eviction; a live re-offer of that branch is now wanted
+      ".Lse_evb_%=:\n\t"
+      "s_mov_b32 s85, %[nfree]\n\t"
+      "s_add_u32 %[nfree], %[nfree], 1\n\t"
+      "s_mov_b32 m0, %[nv]\n\t"
+      "s_add_u32 %[nv], %[nv], 1\n\t"
+      "v_writelane_b32 %[evr], %[fs], m0\n\t"
+      "v_cmp_eq_u32_e64 s[90:91], %[fs], %[c]\n\t"
+      "s_and_b64 s[90:91], s[90:91], %[lb]\n\t"
+      "s_or_b64 %[rb], %[rb], s[90:91]\n\t"
+      "s_branch .Lse_slot_%=\n"
+      ".Lse_tie_%=:\n\t"
+      "s_mov_b32 %[st], 2\n\t"
+      "s_branch .Lse_exit_%=\n"
+      ".Lse_rare_%=:\n\t"
+      "s_mov_b32 %[st], 1\n"
+      ".Lse_exit_%=:\n\t"
+      "s_not_b64 %[done], s[80:81]"
+      : [my] "+v"(myslot), [evr] "+v"(evr), [bat] "+v"(bat), [sv0] "+v"(sv0), [ss0] "+v"(ss0), [sv1] "+v"(sv1),
+        [ss1] "+v"(ss1), [nc] "+s"(NC), [rb] "+s"(RB), [done] "+s"(done), [fv] "+s"(fv), [fs] "+s"(fs),
+        [floc] "+s"(floc), [ft] "+s"(ftied), [nfree] "+s"(nfree), [nv] "+s"(nv), [k] "=&s"(k), [st] "=&s"(st),
+        [cnt] "+s"(cnt)
+      : [s] "v"(s), [c] "v"(c), [sl] "v"(sl), [lb] "s"(LB), [nb] "s"(nb)
+      : "memory", "vcc", "m0", "s80", "s81", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93",
+        "s94", "s95", "v232", "v242");
   return st;
 }
 
@@ -2462,6 +2630,23 @@ constexpr bool kExtLate = CTCX_EXT_LATE != 0;
 #define CTCX_EXT_FIRST 0
 #endif
 constexpr bool kRankFast = CTCX_RANK_FAST != 0;
+// CTCX_SET_MODE: a frame that follows a tie-free one (the helper's ranks of the
+// previous beam: no two equal totals) keeps its full beam as an unordered set in
+// registers instead of the libstdc++ heap.  Without ties the heap's layout
+// decides nothing: every eviction takes the unique minimum and the sorted
+// order is the ranks.  A push is then a register write and a DPP minimum, and
+// the extract is the helper's ranks.  A tie at an eviction, or in the final
+// beam, returns kReplay: the frame runs again on the heap.
+#ifndef CTCX_SET_MODE
+#define CTCX_SET_MODE 0
+#endif
+constexpr bool kSetMode = CTCX_SET_MODE != 0;
+constexpr int kReplay = 5;   // exact_step: decode the frame again with the heap
+constexpr int kTopSet = 3;   // the TopN state of the set mode (after kTopHeap in ctcx_topn.h's enum)
+#ifndef CTCX_SET_ASM
+#define CTCX_SET_ASM 1
+#endif
+constexpr bool kSetAsm = CTCX_SET_ASM != 0;   // the set mode's common events in set_events_f32
 constexpr int kExtFirst = CTCX_EXT_FIRST;   // (A/B: the helper ranks after its pending ring flush)
 constexpr bool kExtBig = CTCX_EXT_BIG != 0;   // large C too: off (cfg4 162.5 -> 169.6 ms, same box; cfg3 unmoved)
 constexpr int kCtlStop = 3, kCtlExt = 7;   // (misc words; both reset per frame)
@@ -2481,7 +2666,8 @@ __device__ CTCX_HELPER_FN void help_rank_extract(CTCX_HCTX cx, CTCX_LDS int* scr
     __builtin_amdgcn_s_sleep(CTCX_EXT_SLEEP);
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  if (ctl_ld(m, kCtlExt) != 1) return;
+  const int ext = ctl_ld(m, kCtlExt);   // 1: wave 0 pops from the heap; 2: its set (kSetMode) waits for the ranks
+  if (kSetMode ? ext == 0 : ext != 1) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 #ifdef CTCX_PHASE_EXTT
   const uint32_t hx0 = (uint32_t)__builtin_amdgcn_s_memtime();
@@ -2507,7 +2693,10 @@ __device__ CTCX_HELPER_FN void help_rank_extract(CTCX_HCTX cx, CTCX_LDS int* scr
         g1 += x[u] > v1;
       }
     }
-    if (__ballot((in0 && v0 != v0) || (in1 && v1 != v1))) return;   // (no order to rank by)
+    if (__ballot((in0 && v0 != v0) || (in1 && v1 != v1))) {   // (no order to rank by)
+      if (kSetMode && ext == 2) __hip_atomic_store(&m[kCtlStop], -1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return;
+    }
     // a tie is two entries of one rank: each entry writes its index at its
     // rank in scr (the gather queue's score plane: free once the grow is
     // over), and of two that collide at least one reads back the other's
@@ -2530,11 +2719,25 @@ __device__ CTCX_HELPER_FN void help_rank_extract(CTCX_HCTX cx, CTCX_LDS int* scr
         e1 += x[u] == v1;
       }
     }
-    if (__ballot((in0 && v0 != v0) || (in1 && v1 != v1))) return;   // (no order to rank by)
+    if (__ballot((in0 && v0 != v0) || (in1 && v1 != v1))) {   // (no order to rank by)
+      if (kSetMode && ext == 2) __hip_atomic_store(&m[kCtlStop], -1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return;
+    }
   }
   if (in0 && e0 > 1) p = g0 < p ? g0 : p;
   if (in1 && e1 > 1) p = g1 < p ? g1 : p;
   p = uni(wave_min(p));
+#ifdef CTCX_PHASE_BIRTH   // (diagnostics: ties in a frame whose previous frame ended without one)
+  if ((cx).prof && threadIdx.x == 64) {
+    const int pp = (int)cx.prof[29];   // the previous frame's p (state, not a sum; 0 at the first frame)
+    if (pp == W) {
+      CTCX_HPC_(cx, 30, 1);
+      CTCX_HPC_(cx, 31, p < W ? 1 : 0);
+    }
+    CTCX_HPC_(cx, 28, p == W ? 1 : 0);
+    cx.prof[29] = (uint64_t)p;
+  }
+#endif
 #ifdef CTCX_PHASE_EXTP   // (diagnostics: the stop the helper found, 16-bit frame counts per range)
   CTCX_HPC(cx, 27, 1ull << (16 * (p <= 2 ? 0 : p < 64 ? 1 : p < 96 ? 2 : 3)));
 #endif
@@ -2561,6 +2764,10 @@ __device__ CTCX_HELPER_FN void help_rank_extract(CTCX_HCTX cx, CTCX_LDS int* scr
     }
   }
 #endif
+  if (kSetMode && ext == 2 && p < W) {   // set mode with a tie: wave 0 replays the frame on the heap
+    __hip_atomic_store(&m[kCtlStop], -1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return;
+  }
   if (p <= 2) return;   // wave 0 pops every position anyway
   if (in0 && g0 < p) cx.sorted[g0] = cx.alias[lane];
   if (in1 && g1 < p) cx.sorted[g1] = cx.alias[lane + 64];
@@ -2620,7 +2827,7 @@ __shared__ int g_sq_dbg[8];   // (diagnostics: the first scored-field mismatch)
 #endif
 template <typename T, int RN, bool BIG, class SC, bool HW, bool SQ>
 __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, bool last, int P, int* n_out,
-                          int* n_leaves, PhaseCtr pc, Tab tb, GQ gq) {
+                          int* n_leaves, PhaseCtr pc, Tab tb, GQ gq, bool setm_in = false) {
   // SQ: the scored gather queue (two-wave kernels, beams <= 128, any C): with
   // the beam full, every chunk of the grow comes from the helper scored
   static_assert(!SQ || (HW && (RN == 1 || (RN == 2 && BIG))), "SQ kernels");
@@ -2722,6 +2929,13 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     st = kTopBottomKnown;
   }
   T bottom = full ? front.v : NI;
+  // the set mode (kSetMode): kernels with the helper's ranks, float beams <= 128
+  constexpr bool kSetK = kSetMode && HW && SQ && RN == 1 && !BIG && sizeof(T) == 4 && !SC::kStateful &&
+                         kExtRank && !kExtLate;
+  const bool setm = kSetK && setm_in && !last && full && W >= kExtMinW && W <= 128;
+  float sv0 = __builtin_inff(), sv1 = __builtin_inff();
+  int ss0 = -1, ss1 = -1, floc = 0;
+  bool ftied = false;
 
   // grow (decoder.h:146-209): offers in (branch order, label order), 64 per
   // chunk.  Within a chunk the entry writes, the resets of evicted branch
@@ -3427,6 +3641,106 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
     int nev = 0;
     uint64_t done = 0;
     while (true) {
+      if (kSetK && st == kTopSet) {
+        // the set mode's events: the selections and bookkeeping of
+        // heap_events_f32 and its caller's re-offer path, the push a register
+        // write and the new front a DPP minimum
+        const uint64_t liveM = __ballot(live);
+        uint64_t NC = liveM & ~isbm, LB = liveM & isbm, RB = LB & __ballot(cev);
+        float fv = (float)front.v;
+        int fs = front.s;
+        int nfree = nextfree;
+        int nv = uni(nev);
+        bool tie_ev = false;
+#ifdef CTCX_PHASE_SET
+        const uint64_t tsl0 = pc ? __builtin_amdgcn_s_memtime() : 0;
+        int npush = 0;
+#endif
+        int ftied_i = ftied ? 1 : 0;
+        for (;;) {
+          fv = uni(fv); fs = uni(fs); nfree = uni(nfree); nv = uni(nv);
+          if constexpr (kSetK && kSetAsm) {
+            int ka, cnt = 0;
+            int fl = floc;
+            const int est = set_events_f32((float)s, c, sl, sv0, ss0, sv1, ss1, myslot, evr, bat, NC, RB, done, LB,
+                                           fv, fs, fl, ftied_i, nfree, nv, uni(nb), ka, cnt);
+            floc = uni(fl);
+#ifdef CTCX_PHASE_SET
+            npush += uni(cnt);
+#endif
+            if (est == 0) break;
+            if (est == 2) { tie_ev = true; break; }
+            ftied = ftied_i != 0;
+          }
+          const uint64_t gtM = __ballot(s > fv);
+          const uint64_t m = ((gtM & NC) | RB) & ~done;
+          if (m == 0) break;
+          const int k = (int)__builtin_ctzll(m);
+          int slot;
+          if ((kSetK && kSetAsm) || ((LB >> k) & 1ull)) {
+            // a re-offered branch child: was k's turn skipped?
+            if ((__ballot(!(bt > bat)) >> k) & 1ull) {
+              const uint64_t keepM = lowmask(bcast(sl, k));   // that branch and every later one
+              NC &= keepM; LB &= keepM; RB &= keepM;
+              stop = true;
+              continue;
+            }
+            done = m ^ (m - 1ull);
+            const int kc = bcast(c, k);
+            if (!((gtM >> k) & 1ull)) {
+              // re-offered evicted branch rejected -> deactivated (decoder.h:200-205)
+              evr = writelane(evr, kc | kDeactRec, nv);
+              dz = true;
+              nv += 1;
+              const uint64_t dm = ~__ballot(i == kc);
+              NC &= dm; LB &= dm; RB &= dm;
+              continue;
+            }
+            if (ftied) { tie_ev = true; break; }
+            if (fs < nb) {   // accepted: the branch's entry keeps its slot
+              evr = writelane(evr, fs, nv);
+              nv += 1;
+              RB |= LB & __ballot(c == fs);
+            }
+            slot = kc;
+          } else {
+            done = m ^ (m - 1ull);
+            if (ftied) { tie_ev = true; break; }
+            slot = fs;
+            if (fs < nb) {   // the evicted front is a branch's entry: a fresh slot
+              slot = nfree;
+              nfree += 1;
+              evr = writelane(evr, fs, nv);
+              nv += 1;
+              RB |= LB & __ballot(c == fs);
+            }
+          }
+          slot = uni(slot);
+          const float k_s = bcast((float)s, k);
+          myslot = (myslot == fs) ? -1 : myslot;
+          myslot = (lane == k) ? slot : myslot;
+          set_put(sv0, ss0, sv1, ss1, floc, k_s, slot);
+          set_front(sv0, ss0, sv1, ss1, fv, fs, floc, ftied);
+          ftied_i = ftied ? 1 : 0;
+          bat = (sl > k) ? (T)fv : bat;
+#ifdef CTCX_PHASES
+          if (pc) pc[6] += 1;
+#endif
+#ifdef CTCX_PHASE_SET
+          ++npush;
+#endif
+        }
+#ifdef CTCX_PHASE_SET
+        if (pc) { pc[23] += __builtin_amdgcn_s_memtime() - tsl0; pc[18] += npush; }
+#endif
+        if (tie_ev) return kReplay;   // an eviction among equal minima: the heap decides
+        nev = nv;
+        front.v = (T)fv;
+        front.s = fs;
+        bottom = front.v;
+        nextfree = nfree;
+        break;
+      }
       if ((RN == 1 || RN == 2) && st == kTopHeap && W >= 2) {
         // HEAP_SORTED, beams up to 128 (the mask form of the loop below, same
         // decisions): new-child lanes wanting in (NC: live, not a branch) are
@@ -3715,7 +4029,17 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
           if (full && lane == 0) he[1].v = NI;
           if (lane == 0) he_st(he, n + 1, nv);
           ++n;
-          if (n == W + 1) {
+          if (kSetK && setm && n == W + 1) {
+            // the set: positions 2..W+1 (the front at 1 was evicted)
+            if (lane < W) { sv0 = (float)he[lane + 2].v; ss0 = he[lane + 2].s; }
+            if (lane + 64 < W) { sv1 = (float)he[lane + 66].v; ss1 = he[lane + 66].s; }
+            float fv0;
+            int fs0;
+            set_front(sv0, ss0, sv1, ss1, fv0, fs0, floc, ftied);
+            front.v = (T)fv0;
+            front.s = fs0;
+            st = kTopSet;
+          } else if (n == W + 1) {
 #ifdef CTCX_FASTLOOP_PROF
             const uint64_t q4 = __builtin_amdgcn_s_memtime();
 #endif
@@ -3785,6 +4109,18 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
   // heap's copy, then kCtlExt, both ahead of kCtlDone
   constexpr bool kExt = HW && SQ && RN == 1 && kExtRank && (kExtBig || !BIG);
   const bool ext_rank = kExt && st == kTopHeap && W >= kExtMinW;
+  if constexpr (kSetK) {
+    if (st == kTopSet) {   // the set's copy; kCtlExt 2: the helper publishes its ranks' verdict
+      CTCX_LDS float* xv = (CTCX_LDS float*)cx.newpos;
+      const int W4 = (W + 3) & ~3;
+      if (lane < W) { xv[lane] = sv0; cx.alias[lane] = ss0; }
+      else if (lane < W4) xv[lane] = __builtin_nanf("");
+      if (lane + 64 < W) { xv[lane + 64] = sv1; cx.alias[lane + 64] = ss1; }
+      else if (lane + 64 < W4) xv[lane + 64] = __builtin_nanf("");
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+      if (lane == 0) __hip_atomic_store(&cx.misc[kCtlExt], 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
   if constexpr (kExt) {
     if (ext_rank) {
       CTCX_LDS float* xv = (CTCX_LDS float*)cx.newpos;
@@ -3829,7 +4165,24 @@ __device__ __forceinline__ int exact_step(Ctx<T>& cx, int buf, int nb, T norm, b
   }
   // Extract() of the next frame (decoder.h:84): sort_heap, or std::sort
   int nout;
-  if (RN == 1 && st == kTopHeap && W >= 2) {
+  if (kSetK && st == kTopSet) {
+    // the set mode: the helper's ranks place every position, unless two
+    // totals tie (-1: the heap's pops decide their order -- replay)
+    int p = 0;
+    uint64_t tw = 0;
+    for (int spin = 0;; ++spin) {
+      p = uni(__hip_atomic_load(&cx.misc[kCtlStop], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+      if (p != 0) break;
+      if (ctl_ld(cx.misc, kCtlDead) != 0 || wait_expired(spin, tw)) {   // never in a correct run
+        cx.tabdead = 1;
+        __hip_atomic_store(&cx.misc[kCtlDead], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return 1;   // the literal path decodes this frame
+      }
+      __builtin_amdgcn_s_sleep(CTCX_EXT_SLEEP);
+    }
+    if (p != W) return kReplay;
+    nout = W;
+  } else if (RN == 1 && st == kTopHeap && W >= 2) {
     // sort_heap in mask form (beams up to 128).  pop_heap(len) parks the old
     // front at position len - 1, which no later sift reads: the slot goes
     // straight into a register lane (position p: lane p of srt[p >> 6])
@@ -4659,6 +5012,7 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
   int nb = 1;
   int literal_steps = 0;
   int why_nf = 0, why_fill = 0, dup_frames = 0;
+  bool tiefree = false;  // the previous frame's beam had no tie (kSetMode)
   bool dup = false;   // this frame's beam holds an entry twice (literal frames only)
   int n_leaves = 1;
   __syncthreads();
@@ -4743,9 +5097,14 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
     int nl_fast = 0;
     uint64_t t1 = prof ? __builtin_amdgcn_s_memtime() : 0;
     if (prof) pc[0] += t1 - t0;
+    bool again = false;
+    int pass = 0;
+    [[maybe_unused]] const bool set_try = tiefree;
+    do {
 #ifndef CTCX_GSTATE   // the global-state tier replays every frame literally
     if (!prm.force_literal && !dup)
-      why = exact_step<T, RN, BIG, SC, HW, SQ>(cx, buf, nb, norm, last, prm.P, &n, &nl_fast, prof ? pc : PhaseCtr{nullptr}, tb, gq);
+      why = exact_step<T, RN, BIG, SC, HW, SQ>(cx, buf, nb, norm, last, prm.P, &n, &nl_fast, prof ? pc : PhaseCtr{nullptr}, tb, gq,
+                                               pass == 0 && tiefree);
 #endif
     if constexpr (HW) {
       // wave 0's result for both waves; the helper stops if the grow ended
@@ -4769,6 +5128,24 @@ __global__ __launch_bounds__(HW ? 128 : 64) void ctcx_beam_decode(DecodeParams<T
       n = uni(cx.misc[5]);
       nl_fast = uni(cx.misc[6]);
     }
+    // a set-mode frame that met a tie (kReplay): both waves decode it again on
+    // the heap, from the frame's start (the roll restores every branch entry)
+    again = kSetMode && HW && why == kReplay;
+    if (again) {
+      if (tid < 3) cx.misc[kCtlReady + tid] = 0;
+      if (tid == 3) cx.misc[kCtlBot] = (int)0xff800000u;   // -inf
+      if (tid == 4) cx.misc[kCtlExt] = 0;
+      if (tid == 5) cx.misc[kCtlStop] = 0;
+      __syncthreads();
+      ++pass;
+    }
+    } while (again);
+    // the next frame may keep a set if this one's beam has no tie (the
+    // helper's ranks: kCtlStop == W)
+    if constexpr (kSetMode && HW) tiefree = uni(cx.misc[kCtlStop]) == cx.W;
+#ifdef CTCX_PHASE_SET   // (diagnostics: frames tried in the set mode, and replayed)
+    if (prof) { pc[16] += set_try ? 1 : 0; pc[17] += pass; }
+#endif
     __syncthreads();
     uint64_t t2 = prof ? __builtin_amdgcn_s_memtime() : 0;
     const bool ok = (why == 0);

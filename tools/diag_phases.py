@@ -85,4 +85,10 @@ if os.environ.get("CTCX_DIAG_EXTT"):   # (a build with -DCTCX_PHASE_EXTT: when t
 if os.environ.get("CTCX_DIAG_EXTT"):
     print("  helper: kCtlDone seen %.0f cycles after wave 0's extract start (all frames it ranks), rank to publish %.0f"
           % (m[24] / max(1.0, m[26]), m[27] / max(1.0, m[26])))
+if os.environ.get("CTCX_DIAG_BIRTH"):   # (a build with -DCTCX_PHASE_BIRTH)
+    print("  ties: frames ending without a tie %.3f; after such a frame, frames ending with one %.4f (of %.0f per item)"
+          % (m[28] / fr, m[31] / max(1.0, m[30]), m[30]))
+if os.environ.get("CTCX_DIAG_SET"):   # (a build with -DCTCX_PHASE_SET -DCTCX_SET_MODE=1)
+    print("  set mode: frames tried %.3f, replayed on the heap %.4f (of frames); set pushes %.1f per frame, %.0f cycles"
+          " each (in the set loop)" % (m[16] / fr, m[17] / fr, m[18] / fr, m[23] / max(1.0, m[18])))
 
