@@ -1899,6 +1899,19 @@ __device__ __forceinline__ void wsync() {
 #define CTCX_HELPER_FN __forceinline__
 #define CTCX_HCTX const Ctx<T>&
 #endif
+// ... and the unscored gather queue's helper (help_gather_chunks: large C,
+// beams of 129..256, cfg5's kernel) alone: cfg5 -0.4% (1457.0 vs 1462.8 ms,
+// profiles/r6s_ab_helper_call_gq.txt), within what placement moves: off
+#ifndef CTCX_HELPER_CALL_GQ
+#define CTCX_HELPER_CALL_GQ 0
+#endif
+#if CTCX_HELPER_CALL || CTCX_HELPER_CALL_GQ
+#define CTCX_HELPER_FN_GQ __attribute__((noinline))
+#define CTCX_HCTX_GQ Ctx<T>
+#else
+#define CTCX_HELPER_FN_GQ __forceinline__
+#define CTCX_HCTX_GQ const Ctx<T>&
+#endif
 constexpr int kTabSlots = CTCX_TAB_SLOTS;   // chunk slots in the ring
 // A hand-over wait gives up after ~1 s of the constant 100 MHz clock
 // (s_memrealtime), whatever the shader clock or the SIMD's other work: only a
@@ -2780,7 +2793,7 @@ __device__ CTCX_HELPER_FN void help_rank_extract(CTCX_HCTX cx, CTCX_LDS int* scr
 }
 
 template <typename T>
-__device__ CTCX_HELPER_FN void help_gather_chunks(CTCX_HCTX cx, GQ q, int buf, int nb, T norm, T pmax, T bottom,
+__device__ CTCX_HELPER_FN_GQ void help_gather_chunks(CTCX_HCTX_GQ cx, GQ q, int buf, int nb, T norm, T pmax, T bottom,
                                                    int lead) {
   const int lane = threadIdx.x & 63;
   CTCX_LDS int* m = cx.misc;
