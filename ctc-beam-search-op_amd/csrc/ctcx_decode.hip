@@ -1104,6 +1104,25 @@ constexpr bool kBatLazy = CTCX_BAT_LAZY != 0;
 #else
 #define CTCX_EVCNT ""
 #endif
+// CTCX_HE_B64=1: the push's two node stores as ds_write_b64 (one 16-lane-group
+// access each, conflict-free over the lanes' consecutive dummy slots) instead
+// of ds_write2_b32 (two 32-lane accesses, banks (a/4) mod 32: lanes j and
+// j + 16 collide on their dummies); the min child then lives in the even
+// pair v[238:239] and the path mask in v237 (same clobbers)
+#ifndef CTCX_HE_B64
+#define CTCX_HE_B64 0
+#endif
+#if CTCX_HE_B64
+#define CTCX_HEV_CV "v238"
+#define CTCX_HEV_CS "v239"
+#define CTCX_HEV_BT "v237"
+#define CTCX_HEV_STORES "ds_write_b64 v237, v[238:239]\n\tds_write_b64 v236, v[240:241]\n\t"
+#else
+#define CTCX_HEV_CV "v237"
+#define CTCX_HEV_CS "v238"
+#define CTCX_HEV_BT "v239"
+#define CTCX_HEV_STORES "ds_write2_b32 v239, v237, v238 offset1:1\n\tds_write2_b32 v236, v240, v241 offset1:1\n\t"
+#endif
 __device__ __forceinline__ int heap_events_f32(float s, int c, int sl, unsigned anc, unsigned req, unsigned aj,
                                                unsigned al, unsigned ar, unsigned dum, int& myslot, int& evr,
                                                float& bat, uint64_t& NC, uint64_t& RB, uint64_t& done, uint64_t LB,
@@ -1144,14 +1163,14 @@ __device__ __forceinline__ int heap_events_f32(float s, int c, int sl, unsigned 
       "s_waitcnt lgkmcnt(0)\n\t"
       "v_cmp_ngt_f32_e64 s[92:93], v234, v232\n\t"         // pickR = !(R > L)
       "v_mov_b64_e32 v[240:241], s[84:85]\n\t"
-      "v_cndmask_b32_e64 v237, v232, v234, s[92:93]\n\t"   // cv
-      "v_cndmask_b32_e64 v238, v233, v235, s[92:93]\n\t"   // cs
-      "v_bitop3_b32 v239, s92, %[req], %[anc] bitop3:0x28\n\t"
-      "v_cmp_lt_f32_e64 s[96:97], s84, v237\n\t"           // gt: min child > v
+      "v_cndmask_b32_e64 " CTCX_HEV_CV ", v232, v234, s[92:93]\n\t"   // cv
+      "v_cndmask_b32_e64 " CTCX_HEV_CS ", v233, v235, s[92:93]\n\t"   // cs
+      "v_bitop3_b32 " CTCX_HEV_BT ", s92, %[req], %[anc] bitop3:0x28\n\t"
+      "v_cmp_lt_f32_e64 s[96:97], s84, " CTCX_HEV_CV "\n\t"           // gt: min child > v
       "v_cndmask_b32_e64 v236, %[al], %[ar], s[92:93]\n\t" // the min child's address
-      "v_readfirstlane_b32 s86, v237\n\t"                  // c0: the root's min child
-      "v_cmp_eq_u32_e64 s[94:95], 0, v239\n\t"             // onp: on the root's min-child path
-      "v_readfirstlane_b32 s87, v238\n\t"
+      "v_readfirstlane_b32 s86, " CTCX_HEV_CV "\n\t"                  // c0: the root's min child
+      "v_cmp_eq_u32_e64 s[94:95], 0, " CTCX_HEV_BT "\n\t"             // onp: on the root's min-child path
+      "v_readfirstlane_b32 s87, " CTCX_HEV_CS "\n\t"
       "v_cndmask_b32_e64 v236, v236, %[aj], s[96:97]\n\t"  // v lands on the stop (gt) or its min child
       "s_and_b32 s98, s92, %[k31]\n\t"
       "s_bitcmp1_b32 s96, 0\n\t"                           // keep: v stays at the root
@@ -1167,10 +1186,9 @@ __device__ __forceinline__ int heap_events_f32(float s, int c, int sl, unsigned 
       "s_andn2_b64 s[94:95], s[94:95], s[90:91]\n\t"       // live: path nodes at or above the stop
       "s_andn2_b64 s[90:91], s[94:95], s[96:97]\n\t"       // up: takes its min child
       "s_lshl_b64 s[94:95], 1, s86\n\t"                    // the stop
-      "v_cndmask_b32_e64 v239, %[dum], %[aj], s[90:91]\n\t"
+      "v_cndmask_b32_e64 " CTCX_HEV_BT ", %[dum], %[aj], s[90:91]\n\t"
       "v_cndmask_b32_e64 v236, %[dum], v236, s[94:95]\n\t"
-      "ds_write2_b32 v239, v237, v238 offset1:1\n\t"
-      "ds_write2_b32 v236, v240, v241 offset1:1\n\t"
+      CTCX_HEV_STORES
       "ds_read_b128 v[232:235], %[al]\n\t"                 // the next push's child pairs
       CTCX_BAT_C
       "s_and_b64 s[88:89], s[88:89], %[nc]\n\t"
