@@ -15,4 +15,5 @@ for P in "$A" "$B"; do
   (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc $P -d $O/sq_${CFG}_$n -o run --output-format csv -- python3 $R/bench.py --config $CFG --steps 1 --warmup 0 --no-cpu --no-host-io --no-strong > $O/sq_${CFG}_$n.log 2>&1) || exit 30
 done
 python3 $R/tools/sq_summary.py $O/sq_${CFG}_1/run_counter_collection.csv $O/sq_${CFG}_2/run_counter_collection.csv > $O/sq_${CFG}.txt || exit 31
+if [ -n "$SQ_KERNEL2" ]; then SQ_KERNEL=$SQ_KERNEL2 python3 $R/tools/sq_summary.py $O/sq_${CFG}_1/run_counter_collection.csv $O/sq_${CFG}_2/run_counter_collection.csv > $O/sq_${CFG}_k2.txt || exit 32; fi
 echo "[$(date +%T)] done" >> $O/steps.log

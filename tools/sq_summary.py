@@ -2,14 +2,17 @@
 counter_collection CSVs, any number of passes) and prints the instruction mix
 and wait shares per wave.  usage: sq_summary.py pass1.csv [pass2.csv ...]"""
 import csv
+import os
 import sys
 from collections import defaultdict
+
+KERNEL = os.environ.get("SQ_KERNEL", "ctcx_beam_decode")   # substring of the kernel name
 
 tot = defaultdict(float)
 disp = defaultdict(set)
 for path in sys.argv[1:]:
     for r in csv.DictReader(open(path)):
-        if "ctcx_beam_decode" not in r["Kernel_Name"]:
+        if KERNEL not in r["Kernel_Name"]:
             continue
         tot[r["Counter_Name"]] += float(r["Counter_Value"])
         disp[r["Counter_Name"]].add(r["Dispatch_Id"])
