@@ -5990,6 +5990,10 @@ constexpr int kFactsCompact = CTCX_FACTS_COMPACT;
 #define CTCX_FACTS_INTERP 0
 #endif
 constexpr bool kFactsInterp = CTCX_FACTS_INTERP != 0;   // the top set's threshold by interpolation search
+#ifndef CTCX_FACTS_BALLOT
+#define CTCX_FACTS_BALLOT 0
+#endif
+constexpr bool kFactsBallot = CTCX_FACTS_BALLOT != 0;   // the threshold search's counts by ballot popcounts
 // The (rank)-th largest of the n keys of a wave's compact list (rank <= n):
 // MSB-first radix select, 8-bit digits, a 256-bin LDS histogram per pass.
 // Every key lies in [klo, khi], so the bits above their highest differing bit
@@ -6280,12 +6284,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CTCX_FACTS_
       // list, its outside maximum taken from the registers), or a list past its
       // capacity (tau bisected over the row's keys, S from the registers)
       auto cnt_ge = [&](unsigned tau) __attribute__((always_inline)) {
-        int c2 = 0;
+        if constexpr (kFactsBallot) {
+          // one compare per key on the vector unit, the counting on the scalar
+          // unit (a ballot's popcount per key): the kernel is VALU issue-bound
+          int c2 = 0;
 #pragma unroll
-        for (int u = 0; u < NV; ++u)
+          for (int u = 0; u < NV; ++u)
 #pragma unroll
-          for (int c = 0; c < 4; ++c) c2 += k[u][c] >= tau ? 1 : 0;
-        return uni(wave_sum_dpp(c2));
+            for (int c = 0; c < 4; ++c) c2 += __builtin_popcountll(__ballot(k[u][c] >= tau));
+          return c2;
+        } else {
+          int c2 = 0;
+#pragma unroll
+          for (int u = 0; u < NV; ++u)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) c2 += k[u][c] >= tau ? 1 : 0;
+          return uni(wave_sum_dpp(c2));
+        }
       };
       if constexpr (!kRadix) n = cnt_ge(kt);
       unsigned tau = kt;
